@@ -1,0 +1,222 @@
+"""ctypes wrapper of the CPU oracle (liboracle) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / timed CPU baseline.  The product package
+(genome-weaver-align_amd/) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "libgwa_oracle.so")
+
+
+class OrcConfig(ctypes.Structure):
+    # mirrors AlignmentConfig / AlignmentScoreConfig defaults (A/AlignmentConfig.java:40-72,
+    # A/AlignmentScoreConfig.java:37-77)
+    _fields_ = [("k", ctypes.c_float)] + [(n, ctypes.c_int32) for n in (
+        "strategy", "report_type", "top_l", "num_gap_open", "num_gap_ext", "num_split", "match",
+        "mismatch", "gap_open", "gap_ext", "split_open", "indel_end_skip", "band_width")]
+
+    @classmethod
+    def default(cls, **kw):
+        c = cls(0.1, 0, 0, 5, 1, 4, 1, 1, 3, 11, 4, 11, 5, 31)
+        for k, v in kw.items():
+            setattr(c, k, v)
+        return c
+
+
+class OrcStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "fm_searches", "quick_steps", "rank_calls", "states", "max_heap", "hits", "sw", "max_hit_list")]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        L.orc_last_error.restype = ctypes.c_char_p
+        L.orc_index_from_fasta.restype = ctypes.c_void_p
+        L.orc_index_from_fasta.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
+        L.orc_index_from_sequence.restype = ctypes.c_void_p
+        L.orc_index_from_sequence.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_index_from_arrays.restype = ctypes.c_void_p
+        L.orc_index_from_arrays.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_index_free.argtypes = [ctypes.c_void_p]
+        L.orc_index_size.restype = ctypes.c_int64
+        L.orc_index_size.argtypes = [ctypes.c_void_p]
+        L.orc_index_sa.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.orc_index_bwt.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.orc_sam_header.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_align.argtypes = [ctypes.c_void_p, ctypes.POINTER(OrcConfig), ctypes.c_uint32, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+        L.orc_align_mode.argtypes = L.orc_align.argtypes + [ctypes.c_int]
+        L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_align_block_detailed.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                               ctypes.c_char_p, ctypes.c_int]
+        L.orc_query_mask64.restype = ctypes.c_int64
+        L.orc_query_mask64.argtypes = [ctypes.c_char_p] + [ctypes.c_int] * 6
+        L.orc_backward_search.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                          ctypes.c_int64, ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.POINTER(ctypes.c_int64)]
+        L.orc_staircase_mask64.restype = ctypes.c_int64
+        L.orc_staircase_mask64.argtypes = [ctypes.c_int] * 4
+        L.orc_cigar_merge.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.orc_fast_count.restype = ctypes.c_int64
+        L.orc_fast_count.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+        L.orc_revcomp.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _err():
+    return lib().orc_last_error().decode()
+
+
+class Index:
+    """An oracle FM-index (FMIndexOnGenome + the reference text)."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise RuntimeError("oracle index build failed: " + _err())
+        self.h = handle
+
+    @classmethod
+    def from_fasta(cls, text):
+        b = text.encode() if isinstance(text, str) else text
+        return cls(lib().orc_index_from_fasta(b, len(b)))
+
+    @classmethod
+    def from_sequence(cls, name, seq):
+        return cls(lib().orc_index_from_sequence(name.encode(), seq.encode()))
+
+    @classmethod
+    def from_arrays(cls, codes, names, lengths, sa_f=None, sa_r=None):
+        import numpy as np
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        lengths = np.ascontiguousarray(lengths, dtype=np.int64)
+        arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+        f = np.ascontiguousarray(sa_f, dtype=np.int64) if sa_f is not None else None
+        r = np.ascontiguousarray(sa_r, dtype=np.int64) if sa_r is not None else None
+        h = lib().orc_index_from_arrays(codes.ctypes.data, len(codes), len(names), ctypes.cast(arr, ctypes.c_void_p),
+                                        lengths.ctypes.data, f.ctypes.data if f is not None else None,
+                                        r.ctypes.data if r is not None else None)
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_index_free(self.h)
+            self.h = None
+
+    @property
+    def n(self):
+        return lib().orc_index_size(self.h)
+
+    def sa(self, strand):
+        import numpy as np
+        out = np.zeros(self.n, dtype=np.int64)
+        if lib().orc_index_sa(self.h, strand, out.ctypes.data) != 0:
+            raise RuntimeError(_err())
+        return out
+
+    def bwt(self, strand):
+        import numpy as np
+        out = np.zeros(self.n, dtype=np.uint8)
+        lib().orc_index_bwt(self.h, strand, out.ctypes.data)
+        return out
+
+    def sam_header(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        lib().orc_sam_header(self.h, ctypes.byref(p), ctypes.byref(n))
+        s = ctypes.string_at(p, n.value).decode()
+        lib().orc_free(p)
+        return s
+
+    def records(self, reads, config=None):
+        """AlignmentRecord dump per read: {name: [ (tag, chr, strand, start, end, nm, cigar, x0), ... ]}"""
+        txt = self.align(reads, config, mode=1)
+        out = {}
+        cur = None
+        for line in txt.splitlines():
+            f = line.split("\t")
+            if f[0] == "READ":
+                cur = out.setdefault(f[1], [])
+            else:
+                cur.append((f[0], f[1], int(f[2]), int(f[3]), int(f[4]), int(f[5]), f[6], int(f[7])))
+        return out
+
+    def align(self, reads, config=None, with_stats=False, mode=0):
+        """reads: list of (name, seq, qual-or-None). Returns SAM text (no header)."""
+        n = len(reads)
+        names = (ctypes.c_char_p * n)(*[r[0].encode() for r in reads])
+        seqs = (ctypes.c_char_p * n)(*[r[1].encode() for r in reads])
+        quals = (ctypes.c_char_p * n)(*[(r[2].encode() if r[2] is not None else None) for r in reads])
+        cfg = config or OrcConfig.default()
+        out = ctypes.c_void_p()
+        ln = ctypes.c_uint64()
+        stats = (OrcStats * n)() if with_stats else None
+        rc = lib().orc_align_mode(self.h, ctypes.byref(cfg), n, ctypes.cast(names, ctypes.c_void_p),
+                                  ctypes.cast(seqs, ctypes.c_void_p), ctypes.cast(quals, ctypes.c_void_p),
+                                  ctypes.byref(out), ctypes.byref(ln),
+                                  ctypes.cast(stats, ctypes.c_void_p) if stats is not None else None, mode)
+        if rc != 0:
+            raise RuntimeError("oracle align failed: " + _err())
+        s = ctypes.string_at(out, ln.value).decode()
+        lib().orc_free(out)
+        return (s, stats) if with_stats else s
+
+    def backward_search(self, window, ch, lb, ub):
+        a = ctypes.c_int64()
+        b = ctypes.c_int64()
+        lib().orc_backward_search(self.h, window, ch, lb, ub, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+
+def align_block_detailed(ref, query, k):
+    pos = ctypes.c_int32()
+    nm = ctypes.c_int32()
+    buf = ctypes.create_string_buffer(4096)
+    rc = lib().orc_align_block_detailed(ref.encode(), query.encode(), k, ctypes.byref(pos), ctypes.byref(nm), buf, 4096)
+    if rc < 0:
+        raise RuntimeError(_err())
+    if rc == 1:
+        return None
+    return pos.value, buf.value.decode(), nm.value
+
+
+def query_mask64(query, direction, next_idx, pivot, cursor, ch, margin):
+    return lib().orc_query_mask64(query.encode(), direction, next_idx, pivot, cursor, ch, margin) & (2**64 - 1)
+
+
+def staircase_mask64(m, k, kk, offset):
+    return lib().orc_staircase_mask64(m, k, kk, offset) & (2**64 - 1)
+
+
+def cigar_merge(a, b):
+    buf = ctypes.create_string_buffer(256)
+    lib().orc_cigar_merge(a.encode(), b.encode(), buf, 256)
+    return buf.value.decode()
+
+
+def fast_count(seq, ch, s, e):
+    return lib().orc_fast_count(seq.encode(), ch, s, e)
+
+
+def revcomp(seq):
+    buf = ctypes.create_string_buffer(len(seq) + 16)
+    lib().orc_revcomp(seq.encode(), buf, len(seq) + 16)
+    return buf.value.decode()
