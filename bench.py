@@ -1,0 +1,179 @@
+"""bench.py -- reads/s of the MI355X `align -m bsf` path (BASELINE.json metric).
+
+One step = one pass of the hot path (fm_quickscan + bsf_search tiers) over one batch of synthetic
+100 bp reads already resident in HBM.  Weak scaling: every rank holds a full index replica on its
+own GPU and aligns its own shard; value = total reads of all ranks / max-over-ranks time.
+
+  python bench.py [--gpus N --steps K --warmup W] [--genome hg19|ecoli|<Mbp>] [--reads R]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "genome-weaver-align_amd"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+METRIC = "reads/sec (whole node), 100 bp k≤2 vs hg19, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--genome", default=os.environ.get("GWA_BENCH_GENOME", "hg19"))
+    ap.add_argument("--reads", type=int, default=int(os.environ.get("GWA_BENCH_READS", "0")))
+    ap.add_argument("--k", type=float, default=2.0)
+    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "20000")))
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check", type=int, default=2000, help="reads of step 0 checked against the oracle")
+    args = ap.parse_args()
+
+    import numpy as np
+    import synth
+    import gwa
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+    import torch
+    torch.cuda.set_device(local)
+
+    if args.genome == "hg19":
+        contigs, gname = synth.HG19_CONTIGS, "hg19-size synthetic (i.i.d. ACGT, hg19 contig lengths)"
+    elif args.genome == "ecoli":
+        contigs, gname = synth.ECOLI, "E. coli-size synthetic (4,641,652 bp i.i.d. ACGT)"
+    else:
+        mb = float(args.genome)
+        contigs = [("chr%d" % (i + 1), int(mb * 1e6 / 4)) for i in range(4)]
+        gname = "%g Mbp synthetic (4 contigs, i.i.d. ACGT)" % mb
+    reads_per_step = args.reads or (10_000_000 if args.genome == "hg19" else 1_000_000)
+
+    t0 = time.time()
+    codes, names, lengths = synth.genome(contigs, config_id=1)
+    log("genome %d bp generated in %.1fs" % (len(codes), time.time() - t0))
+    t0 = time.time()
+    gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths, device=local)
+    t_index = time.time() - t0
+    log("index built + resident in HBM: %.1fs, %.2f GB" % (t_index, gi.deviceBytes() / 1e9))
+
+    cfg = gwa.AlignmentConfig(k=args.k)
+    # synthetic 100 bp reads, 0-2 substitutions, shard = rank
+    t0 = time.time()
+    seqs, rn = synth.reads(codes, lengths, reads_per_step, 100, 2, config_id=2, shard=rank)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
+    log("reads generated in %.1fs" % (time.time() - t0))
+    t0 = time.time()
+    batch = gwa.Batch(gi, cfg, reads)
+    log("batch resident in HBM: %.1fs" % (time.time() - t0))
+
+    for _ in range(args.warmup):
+        batch.run()
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = qms = sms = 0.0
+    for _ in range(args.steps):
+        batch.run()
+        st = batch.stats()
+        kms += st.kernel_ms
+        qms += st.quickscan_ms
+        sms += st.search_ms
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt])
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t[0])
+
+    sam, off = batch.results()
+    st = batch.stats()
+    total_reads = reads_per_step * args.steps * world
+    value = total_reads / dt
+
+    # parity spot check of this rank's first reads against the oracle (checker only)
+    parity = None
+    if args.check and rank == 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        t0 = time.time()
+        oi = O.Index.from_arrays(codes, names, lengths, sa_f=gi.suffixArray(0), sa_r=gi.suffixArray(1))
+        t_oidx = time.time() - t0
+        nchk = min(args.check, len(reads))
+        exp = oi.align(reads[:nchk], O.OrcConfig.default(k=args.k))
+        got = sam[:int(off[nchk])]
+        parity = {"reads": nchk, "identical": got == exp}
+        log("parity on %d reads: %s (oracle index %.1fs)" % (nchk, got == exp, t_oidx))
+
+    cpu = None
+    if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        if parity is None:
+            oi = O.Index.from_arrays(codes, names, lengths, sa_f=gi.suffixArray(0), sa_r=gi.suffixArray(1))
+        ns = min(args.cpu_sample, len(reads))
+        t0 = time.perf_counter()
+        oi.align(reads[:ns], O.OrcConfig.default(k=args.k))
+        ct = time.perf_counter() - t0
+        cpu = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port",
+               "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the reference "
+                         "BSF path (oracle/), same index" % ns}
+        log("cpu baseline: %.0f reads/s (%d reads in %.1fs)" % (ns / ct, ns, ct))
+
+    # roofline of the dominant kernel: algorithmic bytes = 64 B per Occ block read (+4 B per SA gather)
+    steps = args.steps
+    q_ms, s_ms = qms / steps, sms / steps
+    q_bytes = 64.0 * st.quick_blocks
+    s_bytes = 64.0 * (st.blocks - st.quick_blocks) + 4.0 * st.sa_reads
+    if q_ms >= s_ms:
+        dom, ach_bytes, dom_ms = "fm_quickscan", q_bytes, q_ms
+    else:
+        dom, ach_bytes, dom_ms = "bsf_search", s_bytes, s_ms
+    achieved = ach_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    out = {
+        "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": "%s; %d x 100 bp reads per GPU per step, 0-2 substitutions, -k %g, -m bsf, besthit"
+                               % (gname, reads_per_step, args.k),
+                   "genome_bp": int(len(codes)), "reads_per_gpu_per_step": reads_per_step,
+                   "parallelism": "reads sharded, index replicated (%d GPU)" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": ach_bytes, "avg_launch_ms": dom_ms},
+        "cpu_baseline": cpu,
+        "detail": {"quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
+                   "fm_searches_per_read": st.fm_searches / reads_per_step,
+                   "quick_steps_per_read": st.quick_steps / reads_per_step,
+                   "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
+                   "mapped": st.n_mapped, "unmapped": st.n_unmapped, "index_build_s": t_index,
+                   "index_gb": gi.deviceBytes() / 1e9, "parity": parity},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    batch.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

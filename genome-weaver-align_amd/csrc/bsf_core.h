@@ -1,0 +1,1174 @@
+// bsf_core.h -- per-lane bidirectional suffix-filter search (BSF, `align -m bsf`), MI355X device code.
+//
+// One read per lane.  Each lane owns a slice of HBM scratch (state arena, binary heap, hit arena,
+// DP history) and runs the reference's best-first search with the exact operation order of
+//   S/BidirectionalSuffixFilter.java:278-477 (AlignmentProcess.align_internal)
+// so that results are bit-identical to the reference (and to the CPU oracle in oracle/).
+// Data layouts are MI355X-native (gwa_layout.h): 64-B Occ blocks, full SA, 96..320-B states.
+//
+// The same source is compiled by hipcc for gfx950 (the product) and, for CPU-side debugging of
+// the kernel logic only, by g++ in tests/ (never a product fallback: the C-ABI requires a GPU).
+#pragma once
+#include <math.h>
+
+#include "gwa_layout.h"
+
+namespace gwa {
+
+// ---- Java arithmetic (JLS 15.19: shift counts masked to 6 bits for long) ----
+GWA_HD int64_t jshl(int64_t x, int64_t s) { return (int64_t)((uint64_t)x << (s & 63)); }
+GWA_HD int64_t jushr(int64_t x, int64_t s) { return (int64_t)((uint64_t)x >> (s & 63)); }
+GWA_HD int popc64(uint64_t x) { return __builtin_popcountll(x); }
+
+// ---------------------------------------------------------------------------------------------
+// Rank on one 64-B Occ block (A/OccurrenceCountTable.java:80-107, A/ACGTSequence.java:456-549)
+// ---------------------------------------------------------------------------------------------
+struct Block {
+  uint32_t cnt[4];
+  uint64_t lo0, lo1, hi0, hi1, n0, n1;
+};
+
+GWA_HD void loadBlock(const OccBlock *occ, uint64_t b, Block &o) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 *p = reinterpret_cast<const u32x4 *>(occ + b);
+  u32x4 a = __builtin_nontemporal_load(p + 0);
+  u32x4 l = __builtin_nontemporal_load(p + 1);
+  u32x4 h = __builtin_nontemporal_load(p + 2);
+  u32x4 n = __builtin_nontemporal_load(p + 3);
+  o.cnt[0] = a.x; o.cnt[1] = a.y; o.cnt[2] = a.z; o.cnt[3] = a.w;
+  o.lo0 = ((uint64_t)l.y << 32) | l.x; o.lo1 = ((uint64_t)l.w << 32) | l.z;
+  o.hi0 = ((uint64_t)h.y << 32) | h.x; o.hi1 = ((uint64_t)h.w << 32) | h.z;
+  o.n0 = ((uint64_t)n.y << 32) | n.x; o.n1 = ((uint64_t)n.w << 32) | n.z;
+#else
+  const OccBlock &B = occ[b];
+  for (int i = 0; i < 4; ++i) o.cnt[i] = B.cnt[i];
+  o.lo0 = B.lo[0]; o.lo1 = B.lo[1]; o.hi0 = B.hi[0]; o.hi1 = B.hi[1]; o.n0 = B.nmask[0]; o.n1 = B.nmask[1];
+#endif
+}
+
+// counts of A,C,G,T,N in bwt[0, i) where i lies in block B (i>>7 == block index)
+GWA_HD void rankAll(const Block &B, uint64_t i, uint64_t out[5]) {
+  const uint32_t r = (uint32_t)(i & 127);
+  const uint64_t m0 = r >= 64 ? ~0ULL : ((1ULL << r) - 1ULL);
+  const uint64_t m1 = r > 64 ? ((1ULL << (r - 64)) - 1ULL) : 0ULL;
+  const uint32_t pLo = popc64(B.lo0 & m0) + popc64(B.lo1 & m1);
+  const uint32_t pHi = popc64(B.hi0 & m0) + popc64(B.hi1 & m1);
+  const uint32_t pT = popc64(B.lo0 & B.hi0 & m0) + popc64(B.lo1 & B.hi1 & m1);
+  const uint32_t pN = popc64(B.n0 & m0) + popc64(B.n1 & m1);
+  const uint32_t cC = pLo - pT, cG = pHi - pT;
+  const uint32_t cA = r - cC - cG - pT - pN;
+  out[0] = (uint64_t)B.cnt[0] + cA;
+  out[1] = (uint64_t)B.cnt[1] + cC;
+  out[2] = (uint64_t)B.cnt[2] + cG;
+  out[3] = (uint64_t)B.cnt[3] + pT;
+  out[4] = i - out[0] - out[1] - out[2] - out[3];
+}
+
+GWA_HD uint64_t rankOne(const Block &B, uint64_t i, int ch) {
+  const uint32_t r = (uint32_t)(i & 127);
+  const uint64_t m0 = r >= 64 ? ~0ULL : ((1ULL << r) - 1ULL);
+  const uint64_t m1 = r > 64 ? ((1ULL << (r - 64)) - 1ULL) : 0ULL;
+  switch (ch) {
+    case 1: return (uint64_t)B.cnt[1] + popc64(B.lo0 & ~B.hi0 & m0) + popc64(B.lo1 & ~B.hi1 & m1);
+    case 2: return (uint64_t)B.cnt[2] + popc64(B.hi0 & ~B.lo0 & m0) + popc64(B.hi1 & ~B.lo1 & m1);
+    case 3: return (uint64_t)B.cnt[3] + popc64(B.hi0 & B.lo0 & m0) + popc64(B.hi1 & B.lo1 & m1);
+    case 0: {
+      uint32_t any = popc64((B.lo0 | B.hi0 | B.n0) & m0) + popc64((B.lo1 | B.hi1 | B.n1) & m1);
+      return (uint64_t)B.cnt[0] + (r - any);
+    }
+    default: {
+      uint64_t o[5];
+      rankAll(B, i, o);
+      return o[4];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-lane search state (SearchState, S/BidirectionalSuffixFilter.java:658-877)
+// ---------------------------------------------------------------------------------------------
+enum : uint8_t { SI_FWD = 0, SI_BWD = 1, SI_BID = 2, SI_EMPTY = 3 };
+enum : uint8_t { M_SIVALID = 4, M_CURVALID = 8, M_NFAVALID = 16 };
+enum : int { D_FORWARD = 0, D_BACKWARD = 1, D_BIFWD = 2 };
+
+template <int R>
+struct DState {
+  uint32_t lb[4], ub[4];  // SiSet primary intervals: F for SI_FWD/SI_BID, B for SI_BWD (valid iff lb<ub)
+  uint32_t curLb, curUb;  // currentSi
+  uint32_t bBase;         // SI_BID: B interval of ch = bBase + sum_{j<ch} width_j + [0, width_ch)
+  int32_t state;          // flags(5) | base(3) | minK(8) | priority(8) | hasHit(1) | clipped(1)  (:664)
+  int32_t nextSplit;      // arena index, -1 = null
+  uint8_t flag, start, end, cursor;  // Cursor (S/Cursor.java:42-47)
+  uint8_t pivot, nrows, kOffset, meta;
+  uint64_t nfa[R];        // ReadAlignmentNFA rows (S/ReadAlignmentNFA.java:60-61)
+};
+
+struct DHit {
+  int32_t chr, pos, matchLength, qStart, qEnd, diff, strand, numHits, next;
+  int32_t cigarOff, cigarLen;
+  int32_t pad;
+};
+
+// per-lane scratch capacities (entries)
+struct Caps {
+  int32_t arena, heap, hits, list, cigar, dpWords, path;
+};
+
+template <int R>
+struct LaneMem {
+  DState<R> *arena;
+  int32_t *heap;
+  DHit *hits;
+  int32_t *list;
+  uint16_t *cigar;
+  uint64_t *dp;
+  uint8_t *path;
+  uint64_t *masks;  // [strand 2][F/R 2][ch 4][block 4]
+};
+
+template <int R>
+GWA_HD size_t laneBytes(const Caps &c) {
+  size_t b = 0;
+  b += sizeof(DState<R>) * (size_t)c.arena;
+  b += 4 * (size_t)c.heap;
+  b += sizeof(DHit) * (size_t)c.hits;
+  b += 4 * (size_t)c.list;
+  b += 2 * (size_t)c.cigar;
+  b = (b + 7) & ~(size_t)7;
+  b += 8 * (size_t)c.dpWords;
+  b += 8 * 64;
+  b += (size_t)c.path;
+  return (b + 255) & ~(size_t)255;
+}
+
+template <int R>
+GWA_HD LaneMem<R> laneMem(uint8_t *base, const Caps &c) {
+  LaneMem<R> L;
+  size_t b = 0;
+  L.arena = (DState<R> *)(base + b); b += sizeof(DState<R>) * (size_t)c.arena;
+  L.heap = (int32_t *)(base + b); b += 4 * (size_t)c.heap;
+  L.hits = (DHit *)(base + b); b += sizeof(DHit) * (size_t)c.hits;
+  L.list = (int32_t *)(base + b); b += 4 * (size_t)c.list;
+  L.cigar = (uint16_t *)(base + b); b += 2 * (size_t)c.cigar;
+  b = (b + 7) & ~(size_t)7;
+  L.dp = (uint64_t *)(base + b); b += 8 * (size_t)c.dpWords;
+  L.masks = (uint64_t *)(base + b); b += 8 * 64;
+  L.path = base + b;
+  return L;
+}
+
+struct Overflow {};  // thrown only on host test builds; device uses status codes
+
+template <int R>
+struct BsfLane {
+  const IndexView &ix;
+  const SearchConfig &cfg;
+  const StairTables &st;
+  LaneMem<R> L;
+  Caps caps;
+  // read
+  const uint8_t *rd;  // original codes 0..4
+  int m, k;
+  bool nReplaced;
+  // search bookkeeping (AlignmentProcess fields, :175-187, :588-592)
+  int minMismatches, maxMatchLength, bestScore;
+  int numFMIndexSearches;
+  int nStates, heapSize, nHits, listSize, nCigar;
+  int status;  // ST_*
+  // instrumentation
+  int quickSteps, blocks, saReads;
+
+  GWA_HD BsfLane(const IndexView &ix_, const SearchConfig &c_, const StairTables &s_, LaneMem<R> L_, Caps caps_)
+      : ix(ix_), cfg(c_), st(s_), L(L_), caps(caps_) {}
+
+  // q[strand][i] after replaceN_withA (S/BidirectionalSuffixFilter.java:281-291): q[1] is the
+  // complement (not the reverse complement) of q[0] (:193); N -> A on both.
+  GWA_HD int q(int strand, int i) const {
+    int c = rd[i];
+    if (c >= 4) return 0;
+    return strand ? 3 - c : c;
+  }
+
+  // ---- FM index primitives (A/FMIndexOnGenome.java:121-225) ----
+  GWA_HD uint64_t occOne(int fm, int ch, uint64_t i) {
+    if (i > ix.N) i = ix.N;
+    Block B;
+    loadBlock(ix.occ[fm], i >> 7, B);
+    ++blocks;
+    return rankOne(B, i, ch);
+  }
+  // two rankACGTN calls; block shared when lb and ub fall in the same 128-position window
+  GWA_HD void rank2(int fm, uint64_t lb, uint64_t ub, uint64_t lo[5], uint64_t hi[5]) {
+    if (lb > ix.N) lb = ix.N;
+    if (ub > ix.N) ub = ix.N;
+    Block B;
+    loadBlock(ix.occ[fm], lb >> 7, B);
+    ++blocks;
+    rankAll(B, lb, lo);
+    if ((ub >> 7) != (lb >> 7)) {
+      loadBlock(ix.occ[fm], ub >> 7, B);
+      ++blocks;
+    }
+    rankAll(B, ub, hi);
+  }
+
+  // ---- SequenceBoundary.translate (A/SequenceBoundary.java:104-121): last offset < textIndex ----
+  GWA_HD int translate(int64_t textIndex, int32_t *chr, int32_t *pos) const {
+    int lo = 0, hi = ix.nContig;  // count of offsets < textIndex
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (ix.contigOff[mid] < textIndex) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == 0) return -1;  // UTGBException
+    *chr = lo - 1;
+    *pos = (int32_t)(textIndex - ix.contigOff[lo - 1]);
+    return 0;
+  }
+
+  // ---- QueryMask (A/QueryMask.java:41-97) ----
+  GWA_HD uint64_t &mask(int strand, int fr, int ch, int b) { return L.masks[((strand * 2 + fr) * 4 + ch) * 4 + b]; }
+  GWA_HD void buildMasks() {
+    const int nb = (m + 63) / 64;
+    for (int s = 0; s < 2; ++s)
+      for (int fr = 0; fr < 2; ++fr)
+        for (int c = 0; c < 4; ++c)
+          for (int b = 0; b < 4; ++b) mask(s, fr, c, b) = 0;
+    for (int s = 0; s < 2; ++s)
+      for (int i = 0; i < m; ++i) {
+        int c = q(s, i);
+        mask(s, 0, c, i >> 6) |= 1ULL << (i & 63);
+        int j = m - i - 1;
+        mask(s, 1, c, j >> 6) |= 1ULL << (j & 63);
+      }
+    (void)nb;
+  }
+  // BitVector.substring64 (A/BitVector.java:106-116) on a pattern mask of m bits
+  GWA_HD int64_t substring64(int strand, int fr, int ch, int64_t start, int64_t end) {
+    const int nb = (m + 63) / 64;
+    int pos = (int)(start / 64);
+    if (pos >= nb) return 0;
+    int64_t range = end - start;
+    int64_t msk = (range >= 64) ? ~0LL : ~jshl(~0LL, range);
+    int64_t offset = start % 64;
+    int64_t low = jushr((int64_t)mask(strand, fr, ch, pos), offset);
+    int64_t high = pos + 1 < nb ? jshl((int64_t)mask(strand, fr, ch, pos + 1) & ~jshl(~0LL, offset), 64 - offset) : 0;
+    return (high | low) & msk;
+  }
+  GWA_HD int64_t patternMask64(int strand, bool isForward, int nextIdx, int pivot, int cursor, int ch, int margin) {
+    int64_t p;
+    if (isForward) {
+      int pos = nextIdx - margin;
+      if (pos < 0) {
+        p = substring64(strand, 0, ch, 0, 64);
+        p = jshl(p, -pos);
+      } else
+        p = substring64(strand, 0, ch, pos, m);
+    } else {
+      int b = m - pivot;
+      int rshift = pivot - cursor - margin;
+      p = substring64(strand, 1, ch, b, b + 64);
+      if (rshift >= 0) p = jushr(p, rshift);
+      else p = jshl(p, -rshift);
+    }
+    return p;
+  }
+  // StaircaseFilter.getStairCaseMask64bit via the host-built table (S/StaircaseFilter.java:91-102)
+  GWA_HD int64_t stairMask(int row, int offset) {
+    const int kk = minMismatches;
+    if (row >= kk + 1) return 0;
+    const int km = st.kmax;
+    uint32_t base = st.base[m];
+    if (base >= 0xFFFFFFFEu) { status = ST_ERROR; return 0; }  // StaircaseFilter ctor throws for this m
+    return (int64_t)st.tab[base + ((size_t)(kk * (km + 1) + row) * (size_t)(m + km + 1) + (size_t)(offset + km))];
+  }
+
+  // ---- Cursor (S/Cursor.java) ----
+  GWA_HD static int cDir(const DState<R> &s) { int d = (s.flag >> 1) & 3; return d == 3 ? D_FORWARD : d; }
+  GWA_HD static bool cFwd(const DState<R> &s) { return cDir(s) != D_BACKWARD; }
+  GWA_HD static int cStrand(const DState<R> &s) { return s.flag & 1; }
+  GWA_HD static int cFrag(const DState<R> &s) { return (int)s.end - (int)s.start; }
+  GWA_HD static int cProcessed(const DState<R> &s) { return cFwd(s) ? (int)s.cursor - (int)s.pivot : (int)s.end - (int)s.cursor; }
+  GWA_HD static int cRemaining(const DState<R> &s) { return cFrag(s) - cProcessed(s); }
+  GWA_HD static int cNextIdx(const DState<R> &s) { return cFwd(s) ? (int)s.cursor : (int)s.cursor - 1; }
+  GWA_HD static int cOffsetOfSearchHead(const DState<R> &s) {
+    int off = (int)s.cursor - (int)s.start;
+    if (cStrand(s) == 1) off = cFrag(s) - off;
+    return off;
+  }
+  GWA_HD static void setCursor(DState<R> &d, int strand, int dir, int start, int end, int cur, int piv) {
+    d.flag = (uint8_t)(strand | (dir << 1));
+    d.start = (uint8_t)start; d.end = (uint8_t)end; d.cursor = (uint8_t)cur; d.pivot = (uint8_t)piv;
+  }
+
+  // ---- SiSet accessors (A/SiSet.java) ----
+  GWA_HD static uint8_t siType(const DState<R> &s) { return s.meta & 3; }
+  GWA_HD static bool siValid(const DState<R> &s) { return (s.meta & M_SIVALID) != 0; }
+  // getForward(ch): returns false for null
+  GWA_HD static bool siGetF(const DState<R> &s, int ch, uint32_t *lb, uint32_t *ub) {
+    uint8_t t = siType(s);
+    if (!siValid(s) || (t != SI_FWD && t != SI_BID)) return false;
+    if (s.lb[ch] >= s.ub[ch]) return false;
+    *lb = s.lb[ch]; *ub = s.ub[ch];
+    return true;
+  }
+  GWA_HD static bool siGetB(const DState<R> &s, int ch, uint32_t *lb, uint32_t *ub) {
+    uint8_t t = siType(s);
+    if (!siValid(s)) return false;
+    if (t == SI_BWD) {
+      if (s.lb[ch] >= s.ub[ch]) return false;
+      *lb = s.lb[ch]; *ub = s.ub[ch];
+      return true;
+    }
+    if (t != SI_BID) return false;
+    if (s.lb[ch] >= s.ub[ch]) return false;
+    uint32_t x = 0;
+    for (int j = 0; j < ch; ++j) x += s.ub[j] - s.lb[j];
+    *lb = s.bBase + x;
+    *ub = s.bBase + x + (s.ub[ch] - s.lb[ch]);
+    return true;
+  }
+  GWA_HD static bool siIsEmpty(const DState<R> &s, int ch) {
+    if (!siValid(s)) return true;  // NullPointerException in the reference; never reached (clipped tails)
+    if (siType(s) == SI_EMPTY) return true;
+    return s.lb[ch] >= s.ub[ch];
+  }
+  GWA_HD void siInit(DState<R> &d, int dir) {  // FMIndexOnGenome.initSet (:117-128)
+    d.meta = (uint8_t)((d.meta & ~3) | M_SIVALID | (dir == D_FORWARD ? SI_FWD : dir == D_BACKWARD ? SI_BWD : SI_BID));
+    for (int c = 0; c < 4; ++c) {
+      d.lb[c] = (uint32_t)ix.C[c];
+      d.ub[c] = (uint32_t)ix.C[c + 1];
+    }
+    d.bBase = 0;
+  }
+
+  // ---- state flags ----
+  GWA_HD DState<R> &S(int i) { return L.arena[i]; }
+  GWA_HD int minK(int s) { return (int)(((uint32_t)S(s).state >> 8) & 0xFF); }
+  GWA_HD void setMinK(int s, int d) { S(s).state &= ~(0xFF << 8); S(s).state |= (d & 0xFF) << 8; }
+  GWA_HD int prio(int s) { return (int)(((uint32_t)S(s).state >> 16) & 0xFF); }
+  GWA_HD bool hasHit(int s) { return (((uint32_t)S(s).state >> 24) & 1) != 0; }
+  GWA_HD bool isClipped(int s) { return (((uint32_t)S(s).state >> 25) & 1) != 0; }
+  GWA_HD bool isFinished(int s) { return (S(s).state & 0x1F) == 0x1F; }
+  GWA_HD int curACGT(int s) { int c = ((uint32_t)S(s).state >> 5) & 7; return c > 4 ? 4 : c; }
+  GWA_HD bool isChecked(int s, int ch) { return (S(s).state & (1 << ch)) != 0; }
+  GWA_HD void updateFlag(int s, int ch) { S(s).state |= 1 << ch; }
+  GWA_HD void updateSplitFlag(int s) { S(s).state |= 1 << 4; }
+  GWA_HD int numSplit(int s) {
+    int n = 0;
+    for (int t = S(s).nextSplit; t >= 0; t = S(t).nextSplit) ++n;
+    return n;
+  }
+
+  GWA_HD int allocState() {
+    if (nStates >= caps.arena) { status = ST_OVERFLOW; return -1; }
+    return nStates++;
+  }
+  GWA_HD static int32_t packState(int ch, int mk, int pr, bool hm) {
+    return ((ch & 7) << 5) | ((mk & 0xFF) << 8) | ((pr & 0xFF) << 16) | ((hm ? 1 : 0) << 24);
+  }
+  // new SearchState(k, null, cursor, priority) (:753-757)
+  GWA_HD int newInitial(int strand, int dir, int start, int end, int cur, int piv, int priority) {
+    int id = allocState();
+    if (id < 0) return -1;
+    DState<R> &d = S(id);
+    d.meta = 0;
+    setCursor(d, strand, dir, start, end, cur, piv);
+    siInit(d, dir);
+    d.curLb = d.curUb = 0;
+    d.state = packState(4, 0, priority, false);
+    d.nextSplit = -1;
+    d.nrows = (uint8_t)(k + 1);
+    d.kOffset = 0;
+    d.meta |= M_NFAVALID;
+    for (int i = 0; i < R; ++i) d.nfa[i] = 0;
+    for (int i = 0; i <= k; ++i) d.nfa[i] = (uint64_t)jshl(1, k + i);  // activateDiagonalStates (:77-84)
+    return id;
+  }
+
+  // SearchState.score / upperBoundOfScore (:781-801), iterative over the split chain
+  GWA_HD int chainScore(int s, bool upper) {
+    int len = 0;
+    for (int t = s; t >= 0; t = S(t).nextSplit) ++len;
+    int sum = 0, i = 0;
+    for (int t = s; t >= 0; t = S(t).nextSplit, ++i) {
+      int ns = len - 1 - i;
+      int nm = minK(t) - ns;
+      int mm = cProcessed(S(t)) + (upper ? cRemaining(S(t)) : 0) - nm;
+      sum += mm * cfg.matchScore - nm * cfg.mismatchPenalty - ns * cfg.splitOpenPenalty;
+    }
+    return sum;
+  }
+  // StateQueue comparator (:141-150)
+  GWA_HD int compare(int a, int b) {
+    int diff = prio(a) - prio(b);
+    if (diff == 0) diff = -(chainScore(a, false) - chainScore(b, false));
+    if (diff == 0) diff = -(cProcessed(S(a)) - cProcessed(S(b)));
+    return diff;
+  }
+  // java.util.PriorityQueue.offer / poll
+  GWA_HD void queueAdd(int e) {
+    if (e < 0) return;
+    if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
+    int kk = heapSize++;
+    while (kk > 0) {
+      int parent = (kk - 1) >> 1;
+      int p = L.heap[parent];
+      if (compare(e, p) >= 0) break;
+      L.heap[kk] = p;
+      kk = parent;
+    }
+    L.heap[kk] = e;
+  }
+  GWA_HD int queuePoll() {
+    if (heapSize == 0) return -1;
+    int s = --heapSize;
+    int result = L.heap[0];
+    int x = L.heap[s];
+    if (s != 0) {
+      int kk = 0, half = heapSize >> 1;
+      while (kk < half) {
+        int child = (kk << 1) + 1;
+        int c = L.heap[child];
+        int right = child + 1;
+        if (right < heapSize && compare(c, L.heap[right]) > 0) c = L.heap[child = right];
+        if (compare(x, c) <= 0) break;
+        L.heap[kk] = c;
+        kk = child;
+      }
+      L.heap[kk] = x;
+    }
+    return result;
+  }
+
+  // ---- FMQuickScan.scanMismatchLocations (S/FMQuickScan.java:66-94) ----
+  struct Scan { uint64_t lb, ub; int numMismatches, lmStart; };
+
+  GWA_HD Scan quickScan(int strand) {
+    const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
+    uint64_t lb = 0, ub = ix.N;
+    int mark = 0, nmm = 0;
+    bool have = false;
+    int lmS = 0, lmE = 0;
+    int i = 0;
+    for (; i < m; ++i) {
+      int ch = q(strand, i);
+      // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
+      // one 64-B block when lb and ub share a 128-position window
+      Block B;
+      loadBlock(ix.occ[fm], lb >> 7, B);
+      ++blocks;
+      uint64_t nlb = ix.C[ch] + rankOne(B, lb, ch);
+      if ((ub >> 7) != (lb >> 7)) {
+        loadBlock(ix.occ[fm], ub >> 7, B);
+        ++blocks;
+      }
+      uint64_t nub = ix.C[ch] + rankOne(B, ub, ch);
+      ++quickSteps;
+      lb = nlb; ub = nub;
+      if (lb >= ub) {
+        nmm++;
+        if (!have || (lmE - lmS) < (i - mark)) { have = true; lmS = mark; lmE = i; }
+        lb = 0; ub = ix.N;
+        mark = i + 1;
+      }
+    }
+    if (!have || (lmE - lmS) < (i - mark)) { lmS = mark; lmE = i; }
+    Scan s;
+    s.lb = lb; s.ub = ub; s.numMismatches = nmm; s.lmStart = lmS;
+    return s;
+  }
+
+  // ---- hits (R/ReadHit.java) ----
+  GWA_HD int newHit(int32_t chr, int32_t pos, int ml, int qs, int qe, int diff, int strand, int cigOff, int cigLen, int numHits) {
+    if (nHits >= caps.hits) { status = ST_OVERFLOW; return -1; }
+    DHit &h = L.hits[nHits];
+    h.chr = chr; h.pos = pos; h.matchLength = ml; h.qStart = qs; h.qEnd = qe; h.diff = diff; h.strand = strand;
+    h.numHits = numHits; h.next = -1; h.cigarOff = cigOff; h.cigarLen = cigLen; h.pad = 0;
+    return nHits++;
+  }
+  GWA_HD int putCigarOp(int type, int len) {
+    if (nCigar >= caps.cigar) { status = ST_OVERFLOW; return -1; }
+    L.cigar[nCigar++] = (uint16_t)((len << 3) | type);
+    return 0;
+  }
+  GWA_HD int hitTotalDiff(int h) {
+    int d = 0;
+    for (int t = h; t >= 0; t = L.hits[t].next) d += L.hits[t].diff + (L.hits[t].next >= 0 ? 1 : 0);
+    return d;
+  }
+  GWA_HD int hitTotalMatch(int h) {
+    int d = 0;
+    for (int t = h; t >= 0; t = L.hits[t].next) d += L.hits[t].matchLength;
+    return d;
+  }
+  GWA_HD int hitTotalScore(int h) {
+    int sc = 0;
+    for (int t = h; t >= 0; t = L.hits[t].next) {
+      const DHit &x = L.hits[t];
+      sc += x.matchLength * cfg.matchScore - x.diff * cfg.mismatchPenalty;
+      if (x.next >= 0) sc -= cfg.splitOpenPenalty;
+    }
+    return sc;
+  }
+  // AlignmentResultHolder.add (:606-628)
+  GWA_HD void resultAdd(int hit) {
+    int newK = hitTotalDiff(hit);
+    int matchLen = hitTotalMatch(hit);
+    int newScore = hitTotalScore(hit);
+    if (newScore > bestScore) {
+      if (matchLen > 0 && newK <= minMismatches) minMismatches = newK;
+      bestScore = newScore;
+    }
+    if (maxMatchLength < matchLen) maxMatchLength = matchLen;
+    int n = 0;
+    for (int i = 0; i < listSize; ++i) {
+      int e = L.list[i];
+      if (hitTotalDiff(e) <= minMismatches && hitTotalMatch(e) >= maxMatchLength) L.list[n++] = e;
+    }
+    if (n >= caps.list) { status = ST_OVERFLOW; listSize = n; return; }
+    L.list[n++] = hit;
+    listSize = n;
+  }
+
+  // ReadHit.sortSplits (R/ReadHit.java:148-182): stable insertion sort of the chain
+  GWA_HD int sortSplits(int head) {
+    if (L.hits[head].next < 0) return head;
+    int arr[8];
+    int n = 0;
+    for (int t = head; t >= 0; t = L.hits[t].next) {
+      if (n >= 8) { status = ST_OVERFLOW; return head; }
+      arr[n++] = t;
+    }
+    const int headStrand = L.hits[head].strand;
+    for (int i = 1; i < n; ++i) {
+      int x = arr[i];
+      int j = i - 1;
+      while (j >= 0) {
+        int c = cmpHit(arr[j], x, headStrand);
+        if (status == ST_ERROR) return head;
+        if (c <= 0) break;
+        arr[j + 1] = arr[j];
+        --j;
+      }
+      arr[j + 1] = x;
+    }
+    for (int i = 0; i + 1 < n; ++i) L.hits[arr[i]].next = arr[i + 1];
+    L.hits[arr[n - 1]].next = -1;
+    return arr[0];
+  }
+  GWA_HD int cmpHit(int a, int b, int headStrand) {
+    const DHit &o1 = L.hits[a];
+    const DHit &o2 = L.hits[b];
+    int diff = 0;
+    if (o1.chr == CHR_NULL || o2.chr == CHR_NULL) {
+      diff = o1.qStart - o2.qStart;
+      if (headStrand != 0) diff = -diff;
+    }
+    if (diff != 0) return diff;
+    if (o1.chr == CHR_NULL || o2.chr == CHR_NULL) { status = ST_ERROR; return 0; }  // NullPointerException
+    // chr.compareTo: contig names are compared through their precomputed lexicographic rank
+    diff = chrRankCmp(o1.chr, o2.chr);
+    if (diff != 0) return diff;
+    return (int)((int64_t)o1.pos - (int64_t)o2.pos);
+  }
+  const int32_t *chrRank = nullptr;  // lexicographic (String.compareTo) rank of each contig name
+  GWA_HD int chrRankCmp(int a, int b) const {
+    auto rk = [&](int c) -> int { return c >= 0 ? chrRank[c] : (c == CHR_EMPTY ? -1 : -2); };
+    return rk(a) - rk(b);
+  }
+
+  // ---- BitParallelSmithWaterman.alignBlockDetailed (A/BitParallelSmithWaterman.java:141-147,335-644) ----
+  // query = q[strand][qs,qe) (reversed for strand 1), ref = T[refStart, refEnd)
+  GWA_HD int refCode(int64_t p) const {
+    uint64_t nb = ix.textN[p >> 6];
+    if ((nb >> (p & 63)) & 1) return 4;
+    return (int)((ix.text2[p >> 5] >> ((p & 31) * 2)) & 3);
+  }
+  // returns 0 ok, 1 null (no alignment), <0 overflow
+  GWA_HD int alignBlockDetailed(int strand, int qs, int qe, int64_t refStart, int64_t refEnd, int *outPos, int *outDiff,
+                                int *cigOff, int *cigLen) {
+    const int w = 64;
+    const int mq = qe - qs;
+    const int kb = cfg.bandWidth;
+    const int bMax = mq + w - 1 >= w ? (mq + w - 1) / w : 1;
+    const int N = (int)(refEnd - refStart);
+    if (bMax > 4 || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || mq + N + 2 > caps.path) { status = ST_OVERFLOW; return -1; }
+    auto qcode = [&](int p) -> int { return strand == 1 ? q(strand, qe - 1 - p) : q(strand, qs + p); };
+    uint64_t peq[4][4];
+    for (int c = 0; c < 4; ++c)
+      for (int b = 0; b < 4; ++b) peq[c][b] = 0;
+    for (int p = 0; p < mq; ++p) peq[qcode(p)][p >> 6] |= 1ULL << (p & 63);
+    uint64_t *vp = L.dp;
+    uint64_t *vn = L.dp + (size_t)bMax * (N + 1);
+    auto VP = [&](int r, int j) -> uint64_t & { return vp[(size_t)r * (N + 1) + j]; };
+    auto VN = [&](int r, int j) -> uint64_t & { return vn[(size_t)r * (N + 1) + j]; };
+    for (int r = 0; r < bMax; ++r)
+      for (int j = 0; j <= N; ++j) { VP(r, j) = 0; VN(r, j) = 0; }
+    for (int r = 0; r < bMax; ++r) { VP(r, 0) = ~0ULL; VN(r, 0) = 0; }
+    int D[4] = {0, 0, 0, 0};
+    D[0] = mq;
+    int scoreBoundary[4];
+    for (int i = 0; i < bMax; ++i) { int v = mq - ((i + 1) * w) + kb; scoreBoundary[i] = v > 0 ? v : 0; }
+    int bCeil = (kb + w - 1) / w;
+    if (bCeil < 1) bCeil = 1;
+    bool have = false;
+    int bestTail = 0, bestDiff = 0;
+    auto alignBlock = [&](int j, int ch, int r, int hin) -> int {
+      uint64_t vpv = VP(r, j), vnv = VN(r, j);
+      uint64_t x = ch < 4 ? peq[ch][r] : 0ULL;
+      if (hin < 0) x |= 1ULL;
+      uint64_t d0 = (((x & vpv) + vpv) ^ vpv) | x | vnv;
+      uint64_t hp = vnv | ~(d0 | vpv);
+      uint64_t hn = d0 & vpv;
+      int hout = (int)((hp >> 63) & 1ULL) - (int)((hn >> 63) & 1ULL);
+      uint64_t hp2 = hp << 1, hn2 = hn << 1;
+      if (hin < 0) hn2 |= 1ULL;
+      if (hin > 0) hp2 |= 1ULL;
+      VP(r, j + 1) = hn2 | ~(d0 | hp2);
+      VN(r, j + 1) = d0 & hp2;
+      return hout;
+    };
+    for (int j = 0; j < N; ++j) {
+      int ch = refCode(refStart + j);
+      int carry = 0;
+      for (int b = 0; b < bCeil; ++b) {
+        int ns = alignBlock(j, ch, b, carry);
+        D[b] += ns;
+        carry = ns;
+      }
+      if (bCeil < bMax && D[bCeil - 1] - carry <= scoreBoundary[bCeil - 1] &&
+          ((ch < 4 && (peq[ch][bCeil] & 1ULL) != 0ULL) || carry < 0)) {
+        VP(bCeil, j) = ~0ULL;
+        VN(bCeil, j) = 0ULL;
+        int ns = alignBlock(j, ch, bCeil, carry);
+        D[bCeil] = D[bCeil - 1] - carry + ns;
+        bCeil++;
+      } else {
+        while (bCeil > 1 && D[bCeil - 1] > scoreBoundary[bCeil - 1] + w) --bCeil;
+      }
+      if (bCeil == bMax) {
+        if (!have) { have = true; bestTail = j; bestDiff = D[bCeil - 1]; continue; }
+        if (bestDiff > D[bCeil - 1]) { bestTail = j; bestDiff = D[bCeil - 1]; }
+      }
+    }
+    (void)bestDiff;
+    if (!have) return 1;
+    // traceback (:515-643); path chars are appended in reverse order into L.path
+    uint8_t *path = L.path;
+    int plen = 0;
+    int row = mq - 1, col = bestTail;
+    int diff = 0, leftMostPos = 0;
+    for (;;) {
+      int pth = 0;  // 0 NONE 1 DIAG 2 DIAG_MM 3 LEFT 4 UP
+      if (col >= 0 && row >= 0) {
+        int block = row / w, offset = row % w;
+        uint64_t vpf = VP(block, col + 1) & (1ULL << offset);
+        uint64_t vnf = VN(block, col + 1) & (1ULL << offset);
+        if (refCode(refStart + col) == qcode(row)) pth = 1;
+        else if (vpf != 0) { pth = 4; diff++; }
+        else if (vnf == 0) { pth = 2; diff++; }
+        else { pth = 3; diff++; }
+      }
+      if (pth == 1 || pth == 2) { path[plen++] = 'M'; leftMostPos = col; col--; row--; }
+      else if (pth == 4) { path[plen++] = 'I'; leftMostPos = col + 1; row--; }
+      else if (pth == 3) { path[plen++] = 'D'; col--; }
+      else {
+        while (col >= 0 || row >= 0) {
+          if (row >= 0) path[plen++] = 'S';
+          col--;
+          row--;
+        }
+        break;
+      }
+    }
+    // cigarStr = reverse(path); leading/trailing S/I/D -> S, I/D subtract from diff
+    int left = 0, right = 0;
+    for (int i = 0; i < plen; ++i) {
+      char t = (char)path[plen - 1 - i];
+      if (t == 'S') left++;
+      else if (t == 'I' || t == 'D') { left++; diff--; }
+      else break;
+    }
+    for (int i = plen - 1; i >= left; --i) {
+      char t = (char)path[plen - 1 - i];
+      if (t == 'S') right++;
+      else if (t == 'I' || t == 'D') { right++; diff--; }
+      else break;
+    }
+    // CIGAR.add(char) over S^left + middle + S^right (A/CIGAR.java:143-156)
+    int off = nCigar;
+    int curT = -1, curL = 0;
+    auto push = [&](int t) {
+      if (t == curT) { curL++; return; }
+      if (curT >= 0 && putCigarOp(curT, curL) < 0) return;
+      curT = t;
+      curL = 1;
+    };
+    for (int i = 0; i < left; ++i) push(4);
+    for (int i = left; i < plen - right; ++i) {
+      char t = (char)path[plen - 1 - i];
+      push(t == 'M' ? 0 : t == 'I' ? 1 : t == 'D' ? 2 : 4);
+    }
+    for (int i = 0; i < right; ++i) push(4);
+    if (curT >= 0) putCigarOp(curT, curL);
+    if (status == ST_OVERFLOW) return -1;
+    *cigOff = off;
+    *cigLen = nCigar - off;
+    *outPos = leftMostPos;
+    *outDiff = diff;
+    return 0;
+  }
+
+  // ---- verify (:496-560); returns hit index, -1 = Java null, -2 = overflow ----
+  GWA_HD int verify(int s) {
+    const DState<R> d = S(s);
+    const int strand = cStrand(d);
+    if (isClipped(s)) {
+      int off = nCigar;
+      if (putCigarOp(4, cFrag(d)) < 0) return -2;
+      int h = newHit(CHR_NULL, -1, 0, d.start, d.end, 0, strand, off, 1, 0);
+      return h < 0 ? -2 : h;
+    }
+    if (!(d.meta & M_CURVALID)) {
+      int h = newHit(CHR_EMPTY, 0, 0, 0, 0, 0, strand, nCigar, 0, 0);  // ReadHit.noHit
+      return h < 0 ? -2 : h;
+    }
+    // FMIndexOnGenome.toCoordinate (A/FMIndexOnGenome.java:227-238) via the full SA
+    const int fm = ~(strand ^ (cFwd(d) ? 0 : 1)) & 1;
+    int64_t seqIndex = fm == 0 ? (int64_t)ix.sa[0][d.curLb] : (int64_t)ix.N - (int64_t)ix.sa[1][d.curLb];
+    ++saReads;
+    int64_t x = seqIndex - cOffsetOfSearchHead(d);
+    const int frag = cFrag(d);
+    int64_t refStart = x - k > 0 ? x - k : 0;
+    int64_t refEnd = x + frag + k < (int64_t)ix.N ? x + frag + k : (int64_t)ix.N;
+    if (refStart > refEnd) { status = ST_ERROR; return -2; }  // IllegalArgumentException in subString
+    int pos = 0, diff = 0, co = 0, cl = 0;
+    int r = alignBlockDetailed(strand, d.start, d.end, refStart, refEnd, &pos, &diff, &co, &cl);
+    if (r < 0) return -2;
+    if (r == 1) {
+      int h = newHit(CHR_EMPTY, 0, 0, 0, 0, 0, strand, nCigar, 0, 0);
+      return h < 0 ? -2 : h;
+    }
+    int32_t chr, p;
+    if (translate(refStart + pos + 1, &chr, &p) != 0) return -1;
+    int h = newHit(chr, p, frag, d.start, d.end, diff, strand, co, cl, (int)(d.curUb - d.curLb));
+    return h < 0 ? -2 : h;
+  }
+
+  // reportAlignment (:562-586); returns false on overflow/error
+  GWA_HD bool reportAlignment(int c) {
+    int al = verify(c);
+    if (al == -2) return false;
+    for (int nx = S(c).nextSplit; nx >= 0; nx = S(nx).nextSplit) {
+      int res = verify(nx);
+      if (res == -2) return false;
+      if (al < 0) { status = ST_ERROR; return false; }
+      L.hits[al].next = res;  // nextHit is never advanced (:567-571)
+    }
+    if (al < 0) { status = ST_ERROR; return false; }
+    if (hitTotalMatch(al) == 0) return true;
+    int newK = hitTotalDiff(al);
+    if (newK > k) return true;
+    setMinK(c, newK);
+    int head = sortSplits(al);
+    if (status == ST_ERROR || status == ST_OVERFLOW) return false;
+    resultAdd(head);
+    return status != ST_OVERFLOW;
+  }
+
+  // ---- ReadAlignmentNFA.nextState (S/ReadAlignmentNFA.java:127-203) ----
+  // returns: -1 null, else (hasMatch, new rows/kOffset written into out)
+  GWA_HD bool nfaNext(const DState<R> &s, int ch, int strand, uint64_t *outRows, int *outH, int *outKOff, bool *hasMatch) {
+    const int height = s.nrows;
+    const int kOff = s.kOffset;
+    const int kk = kOff + height - 1;
+    const int kr = kk - kOff;
+    const int64_t qeq = patternMask64(strand, cFwd(s), cNextIdx(s), s.pivot, s.cursor, ch, kr);
+    const int progress = cProcessed(s);
+    const int frag = cFrag(s);
+    int64_t next[R];
+    int minKwithMatch = kk + 1, minKwithProgress = kk + 1;
+    next[0] = jshl((int64_t)s.nfa[0] & qeq, 1);
+    if (next[0] != 0) { minKwithMatch = 0; minKwithProgress = 0; }
+    next[0] &= stairMask(kOff, progress - kk);
+    for (int i = 1; i < height; ++i) {
+      next[i] = jshl((int64_t)s.nfa[i] & qeq, 1);
+      if (minKwithMatch > kk && next[i] != 0) minKwithMatch = i;
+      next[i] |= (int64_t)s.nfa[i - 1] | jshl((int64_t)s.nfa[i - 1], 1) | jshl(next[i - 1], 1);
+      next[i] &= stairMask(kOff + i, progress - kk);
+      if (minKwithProgress > kk && (next[i] & jshl(1, height)) != 0) minKwithProgress = i;
+    }
+    const int mPos = kk + frag - progress;
+    int rem = -1;
+    bool hm = false;
+    if (mPos < 64) {
+      for (int nm = 0; nm < height; ++nm)
+        if ((next[nm] & jshl(1, mPos)) != 0) { rem = nm; hm = true; break; }
+    }
+    if (!hm) {
+      int mk = minKwithMatch < minKwithProgress ? minKwithMatch : minKwithProgress;
+      if (mk < kk) rem = mk;
+      else return false;
+    }
+    // removeLayersFromAutomaton (:205-215): the OLD rows when nothing is trimmed
+    if (rem == 0) {
+      for (int i = 0; i < height; ++i) outRows[i] = s.nfa[i];
+      *outH = height;
+    } else {
+      int nh = height - rem;
+      for (int h = 0; h < nh; ++h) outRows[h] = (uint64_t)jushr(next[h + rem], 1);
+      *outH = nh;
+    }
+    *outKOff = kOff + rem;
+    *hasMatch = hm;
+    return true;
+  }
+
+  // Cursor.nextSi + FMIndexOnGenome.bidirectionalSearch (S/Cursor.java:182-196, A/FMIndexOnGenome.java:162-191)
+  // writes the resulting SiSet into d (lb/ub/bBase/meta-type)
+  GWA_HD void nextSi(const DState<R> &c, int ch, DState<R> &d) {
+    uint32_t fl = 0, fu = 0, bl = 0, bu = 0;
+    bool hasF = siGetF(c, ch, &fl, &fu);
+    bool hasB = siGetB(c, ch, &bl, &bu);
+    if (cDir(c) == D_BIFWD && (int)c.cursor >= (int)c.end - 1) hasF = false;
+    const int strand = cStrand(c);
+    uint64_t lo[5], hi[5];
+    d.meta = (uint8_t)((d.meta & ~3) | M_SIVALID);
+    if (hasF) {
+      const int fm = strand == 0 ? 1 : 0;
+      rank2(fm, fl, fu, lo, hi);
+      for (int i = 0; i < 4; ++i) {
+        d.lb[i] = (uint32_t)(ix.C[i] + lo[i]);
+        d.ub[i] = (uint32_t)(ix.C[i] + hi[i]);
+      }
+      if (!hasB) { d.meta |= SI_FWD; d.bBase = 0; return; }
+      d.meta |= SI_BID;
+      d.bBase = bl;
+      return;
+    }
+    if (hasB) {
+      const int fm = strand == 0 ? 0 : 1;
+      rank2(fm, bl, bu, lo, hi);
+      for (int i = 0; i < 4; ++i) {
+        d.lb[i] = (uint32_t)(ix.C[i] + lo[i]);
+        d.ub[i] = (uint32_t)(ix.C[i] + hi[i]);
+      }
+      d.meta |= SI_BWD;
+      d.bBase = 0;
+      return;
+    }
+    d.meta |= SI_EMPTY;
+    for (int i = 0; i < 4; ++i) d.lb[i] = d.ub[i] = 0;
+    d.bBase = 0;
+  }
+
+  // SearchState.nextState (:840-852); returns new state index, -1 = null, -2 = overflow
+  GWA_HD int nextState(int c, int ch) {
+    const DState<R> cs = S(c);
+    const int strand = cStrand(cs);
+    uint64_t rows[R];
+    int nh = 0, nko = 0;
+    bool hm = false;
+    // the FM step (next(c, ch)) happens first in the reference (:422-424)
+    DState<R> d;
+    d.meta = 0;
+    nextSi(cs, ch, d);
+    ++numFMIndexSearches;
+    if (!nfaNext(cs, ch, strand, rows, &nh, &nko, &hm)) return -1;
+    int id = allocState();
+    if (id < 0) return -2;
+    // Cursor.next (S/Cursor.java:158-180)
+    int nc = cs.cursor, dir = cDir(cs);
+    if (dir == D_FORWARD) ++nc;
+    else if (dir == D_BACKWARD) --nc;
+    else {
+      if (nc + 1 < cs.end) ++nc;
+      else { dir = D_BACKWARD; nc = cs.pivot; }
+    }
+    setCursor(d, strand, dir, cs.start, cs.end, nc, cs.pivot);
+    uint32_t sl = 0, su = 0;
+    bool sv = dir != D_BACKWARD ? siGetF(cs, ch, &sl, &su) : siGetB(cs, ch, &sl, &su);
+    d.curLb = sv ? sl : 0;
+    d.curUb = sv ? su : 0;
+    if (sv) d.meta |= M_CURVALID;
+    d.meta |= M_NFAVALID;
+    d.state = packState(ch, nko, prio(c), hm);
+    d.nextSplit = cs.nextSplit;
+    d.nrows = (uint8_t)nh;
+    d.kOffset = (uint8_t)nko;
+    for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
+    S(id) = d;
+    return id;
+  }
+
+  // nextStateAfterSplit / nextStateAfterClipping (:803-838); -1 null, -2 overflow
+  GWA_HD int nextStateAfterSplit(int c, bool clip) {
+    updateSplitFlag(c);
+    const int mk = minK(c);
+    if (!(mk < k)) return -1;
+    const DState<R> cs = S(c);
+    // Cursor.split (S/Cursor.java:130-156)
+    int strand = cStrand(cs), dir = cDir(cs);
+    int ld, ls, le, lc, lp, rdr, rs, re, rc, rp;
+    if (dir == D_FORWARD) {
+      ld = dir; ls = cs.start; le = cs.cursor; lc = cs.cursor; lp = cs.pivot;
+      rdr = D_FORWARD; rs = cs.cursor; re = cs.end; rc = cs.cursor; rp = cs.cursor;
+    } else if (dir == D_BACKWARD) {
+      ld = dir; ls = cs.cursor; le = cs.end; lc = cs.cursor; lp = cs.pivot;
+      rdr = D_BACKWARD; rs = cs.start; re = cs.cursor; rc = cs.cursor; rp = cs.start;
+    } else {
+      if (cs.cursor + 1 < cs.end) {
+        ld = dir; ls = cs.start; le = cs.cursor; lc = cs.cursor; lp = cs.pivot;
+        rdr = dir; rs = cs.cursor; re = cs.end; rc = cs.cursor; rp = cs.cursor;
+      } else {
+        ld = D_BACKWARD; ls = cs.start; le = cs.cursor; lc = cs.cursor; lp = cs.pivot;
+        rdr = dir; rs = cs.cursor; re = cs.end; rc = cs.cursor; rp = cs.cursor;
+      }
+    }
+    int a = allocState();
+    if (a < 0) return -2;
+    {
+      DState<R> d = cs;  // currentSi, siTable carried over
+      setCursor(d, strand, ld, ls, le, lc, lp);
+      // ReadAlignmentNFA.nextStateAfterSplit (S/ReadAlignmentNFA.java:107-114)
+      int height = cs.nrows - 1;
+      d.nrows = (uint8_t)(height < 0 ? 0 : height);
+      d.kOffset = (uint8_t)(cs.kOffset + 1);
+      for (int i = 0; i < R; ++i) d.nfa[i] = i < height ? (uint64_t)jshl(1, height + i - 1) : 0;
+      d.state = packState(curACGT(c), mk, prio(c), hasHit(c));
+      d.nextSplit = -1;
+      S(a) = d;
+    }
+    int b = allocState();
+    if (b < 0) return -2;
+    {
+      DState<R> t;
+      t.meta = 0;
+      setCursor(t, strand, rdr, rs, re, rc, rp);
+      t.curLb = t.curUb = 0;
+      t.nextSplit = -1;
+      t.state = packState(4, mk, prio(c), false);
+      if (!clip) {
+        siInit(t, rdr);
+        t.meta |= M_NFAVALID;
+        t.nrows = (uint8_t)(k + 1);
+        t.kOffset = 0;
+        for (int i = 0; i < R; ++i) t.nfa[i] = i <= k ? (uint64_t)jshl(1, k + i) : 0;
+      } else {
+        for (int i = 0; i < 4; ++i) t.lb[i] = t.ub[i] = 0;
+        t.bBase = 0;
+        t.nrows = 0;
+        t.kOffset = 0;
+        for (int i = 0; i < R; ++i) t.nfa[i] = 0;
+        t.state |= 1 << 25;  // updateClippedFlag
+      }
+      S(b) = t;
+    }
+    S(a).nextSplit = b;
+    return a;
+  }
+
+  // SearchState.update (:861-875); -1 = null
+  GWA_HD int update(int self, int oldS, int newS) {
+    if (oldS == self) return newS;
+    int prev = self;
+    while (S(prev).nextSplit != oldS) {
+      prev = S(prev).nextSplit;
+      if (prev < 0) return -1;
+    }
+    S(prev).nextSplit = newS;
+    return self;
+  }
+
+  // ---- AlignmentProcess.align_internal (:278-477), split at the quick scan ----
+  // Phase 1 (fm_quickscan kernel): N check, FMQuickScan on both strands, exact hits.
+  // Returns 1 when the read needs the best-first search; otherwise the result is final.
+  GWA_HD int quickPhase(ScanRes *sr, OutHeader *oh, OutHit *oHits, uint16_t *oCig) {
+    oh->fmSearches = 0;
+    oh->states = 0;
+    oh->searchBlocks = 0;
+    oh->saReads = 0;
+    oh->nChains = oh->nHits = oh->nCigar = 0;
+    oh->status = ST_UNMAPPED;
+    {
+      int countN = 0;
+      for (int i = 0; i < m; ++i) countN += rd[i] == 4;
+      if (countN > k) { finishQuick(oh); return 0; }
+    }
+    Scan sF = quickScan(0);
+    if (sF.numMismatches == 0) { reportExact(sF, 0, oh, oHits, oCig); return 0; }
+    Scan sR = quickScan(1);
+    if (sR.numMismatches == 0) { reportExact(sR, 1, oh, oHits, oCig); return 0; }
+    if (k == 0) { finishQuick(oh); return 0; }
+    sr->nmF = sF.numMismatches; sr->lmF = sF.lmStart;
+    sr->nmR = sR.numMismatches; sr->lmR = sR.lmStart;
+    finishQuick(oh);
+    return 1;
+  }
+  GWA_HD void finishQuick(OutHeader *oh) {
+    oh->quickSteps = quickSteps;
+    oh->blocks = blocks;
+  }
+  // reportExactMatchAlignment (:490-494) + FMIndexOnGenome.toGenomeCoordinate (:258-269):
+  // the single exact ReadHit is the reported BESTHIT/ALLHITS/TOPL result.
+  GWA_HD void reportExact(const Scan &s, int strand, OutHeader *oh, OutHit *oHits, uint16_t *oCig) {
+    finishQuick(oh);
+    oh->saReads = 1;
+    int64_t pos = strand == 0 ? (int64_t)ix.N - (int64_t)ix.sa[1][s.lb] : (int64_t)ix.sa[0][s.lb];
+    if (strand == 0) pos -= m;
+    pos += 1;
+    int32_t chr, p;
+    if (pos < 0 || translate(pos, &chr, &p) != 0) { oh->status = ST_ERROR; return; }
+    OutHit &o = oHits[0];
+    o.chr = chr; o.pos = p; o.matchLength = m; o.qStart = 0; o.qEnd = m; o.diff = 0; o.strand = strand;
+    o.numHits = (int32_t)(s.ub - s.lb); o.next = -1; o.cigarOff = 0; o.cigarLen = 1;
+    oCig[0] = (uint16_t)((m << 3) | 0);
+    oh->chainHead[0] = 0;
+    oh->nChains = 1; oh->nHits = 1; oh->nCigar = 1;
+    oh->status = ST_MAPPED;
+  }
+
+  // Phase 2 (bsf_search kernel): seeds from the quick scans (:318-349) and the queue loop (:352-475)
+  GWA_HD void searchPhase(const ScanRes &sr) {
+    buildMasks();
+    int a = -1, b = -1;
+    if (sr.nmF <= k) {
+      if (sr.lmF != 0 && sr.lmF < m) a = newInitial(0, D_BIFWD, 0, m, sr.lmF, sr.lmF, sr.nmF);
+      else a = newInitial(0, D_FORWARD, 0, m, 0, 0, sr.nmF);
+      if (a < 0) return;
+    }
+    if (sr.nmR <= k) {
+      if (sr.lmR != 0 && sr.lmR < m) b = newInitial(1, D_BIFWD, 0, m, sr.lmR, sr.lmR, sr.nmR);
+      else b = newInitial(1, D_FORWARD, 0, m, 0, 0, sr.nmR);
+      if (b < 0) return;
+    }
+    queueAdd(a);
+    queueAdd(b);
+    const int upper = m * 20;
+    while (heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR) {
+      if (numFMIndexSearches > upper) break;
+      const int base = queuePoll();
+      int c = base;
+      {
+        int nx = c;
+        bool reported = false;
+        while (hasHit(nx) || isClipped(nx) || cRemaining(S(nx)) == 0) {
+          if (S(nx).nextSplit < 0) {
+            if (!reportAlignment(c)) return;
+            reported = true;
+            break;
+          }
+          nx = S(nx).nextSplit;
+        }
+        if (reported) continue;
+        c = nx;
+      }
+      if (isFinished(c)) continue;
+      const int nm = minK(c);
+      if (nm > minMismatches) continue;
+      if (minMismatches - nm < 0) continue;
+      {
+        int ub = chainScore(base, true);
+        if (ub < 0 || ub < bestScore) continue;
+      }
+      const int strand = cStrand(S(c));
+      const int nextBase = q(strand, cNextIdx(S(c)));
+      bool advanced = false;
+      {
+        int ch = nextBase;
+        if (!isChecked(c, ch)) {
+          updateFlag(c, ch);
+          if (!siIsEmpty(S(c), ch)) {
+            int ns = nextState(c, ch);
+            if (ns == -2) return;
+            if (ns >= 0) { queueAdd(update(base, c, ns)); advanced = true; }
+          }
+        }
+      }
+      if (advanced) continue;
+      for (int ch = 0; ch < 4; ++ch) {
+        if (!isChecked(c, ch)) {
+          updateFlag(c, ch);
+          if (!siIsEmpty(S(c), ch)) {
+            int ns = nextState(c, ch);
+            if (ns == -2) return;
+            if (ns >= 0) queueAdd(update(base, c, ns));
+          }
+        }
+      }
+      updateSplitFlag(c);
+      if (numSplit(base) < cfg.numSplit && nm + 1 <= minMismatches) {
+        const int index = cNextIdx(S(c));
+        if (index > cfg.indelEndSkip && m - index >= cfg.indelEndSkip) {
+          int ns = nextStateAfterSplit(c, false);
+          if (ns == -2) return;
+          if (ns >= 0) queueAdd(update(base, c, ns));
+          int cl = nextStateAfterSplit(c, true);
+          if (cl == -2) return;
+          if (cl >= 0) queueAdd(update(base, c, cl));
+        }
+      }
+    }
+  }
+
+  // AlignmentProcess.align (:210-268) minus the record conversion (host side, sam.cpp)
+  GWA_HD void initRead(const uint8_t *codes, int m_) {
+    rd = codes;
+    m = m_;
+    k = getMaximumEditDistance(m);
+    minMismatches = k + 1;
+    maxMatchLength = 0;
+    bestScore = -1;
+    numFMIndexSearches = 0;
+    nStates = heapSize = nHits = listSize = nCigar = 0;
+    status = ST_UNMAPPED;
+    quickSteps = blocks = saReads = 0;
+  }
+  // AlignmentProcess.align (:210-268) after the search: pick the reported chains
+  GWA_HD void writeSearchOutput(OutHeader *oh, OutHit *oHits, uint16_t *oCig, int outHitCap, int outCigCap) {
+    oh->fmSearches = numFMIndexSearches;
+    oh->searchBlocks = blocks;
+    oh->saReads = saReads;
+    oh->states = nStates;
+    oh->nChains = 0;
+    oh->nHits = 0;
+    oh->nCigar = 0;
+    if (status == ST_OVERFLOW || status == ST_ERROR) { oh->status = status; return; }
+    bool hasHitF = minMismatches <= k && listSize > 0;
+    if (!hasHitF) { oh->status = ST_UNMAPPED; return; }
+    int nRep = cfg.reportType == 0 ? 1 : cfg.reportType == 1 ? listSize : (cfg.topL < listSize ? cfg.topL : listSize);
+    if (nRep > 4) { oh->status = ST_OVERFLOW; return; }
+    int nh = 0, ncg = 0;
+    for (int r = 0; r < nRep; ++r) {
+      oh->chainHead[r] = nh;
+      int prevOut = -1;
+      for (int t = L.list[r]; t >= 0; t = L.hits[t].next) {
+        const DHit &h = L.hits[t];
+        if (nh >= outHitCap || ncg + h.cigarLen > outCigCap) { oh->status = ST_OVERFLOW; return; }
+        OutHit &o = oHits[nh];
+        o.chr = h.chr; o.pos = h.pos; o.matchLength = h.matchLength; o.qStart = h.qStart; o.qEnd = h.qEnd;
+        o.diff = h.diff; o.strand = h.strand; o.numHits = h.numHits; o.next = -1;
+        o.cigarOff = (uint16_t)ncg;
+        o.cigarLen = (uint16_t)h.cigarLen;
+        for (int i = 0; i < h.cigarLen; ++i) oCig[ncg++] = L.cigar[h.cigarOff + i];
+        if (prevOut >= 0) oHits[prevOut].next = nh;
+        prevOut = nh;
+        ++nh;
+      }
+    }
+    oh->nChains = nRep;
+    oh->nHits = nh;
+    oh->nCigar = ncg;
+    oh->status = ST_MAPPED;
+  }
+
+  // AlignmentScoreConfig.getMaximumEditDistance (A/AlignmentScoreConfig.java:40-47)
+  GWA_HD int getMaximumEditDistance(int readLength) const {
+    if (cfg.k > 0 && cfg.k < 1) return (int)floor((double)((float)readLength * cfg.k));
+    return (int)cfg.k;
+  }
+};
+
+}  // namespace gwa

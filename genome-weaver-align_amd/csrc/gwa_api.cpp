@@ -1,0 +1,555 @@
+// gwa_api.cpp -- C-ABI implementation (include/gwa.h): index residency in HBM, batch
+// orchestration (quick-scan kernel -> work list -> search kernel tiers), SAM formatting.
+#include "../../include/gwa.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bsf_core.h"
+#include "host_index.h"
+#include "kernels.h"
+#include "sam.h"
+
+using namespace gwa;
+
+static thread_local std::string g_err;
+
+namespace {
+
+struct HipError : std::runtime_error {
+  explicit HipError(const std::string &m) : std::runtime_error(m) {}
+};
+#define HIPCHK(x)                                                                                          \
+  do {                                                                                                     \
+    hipError_t e_ = (x);                                                                                   \
+    if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));                  \
+  } while (0)
+
+template <class T>
+T *devAlloc(size_t n, size_t *acc = nullptr) {
+  void *p = nullptr;
+  size_t b = std::max<size_t>(n * sizeof(T), 64);
+  HIPCHK(hipMalloc(&p, b));
+  if (acc) *acc += b;
+  return (T *)p;
+}
+template <class T>
+T *devUpload(const std::vector<T> &v, hipStream_t s, size_t *acc) {
+  T *p = devAlloc<T>(v.size(), acc);
+  if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  return p;
+}
+
+int fail(const std::string &m) {
+  g_err = m;
+  return -1;
+}
+
+}  // namespace
+
+struct gwa_index {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  HostIndex host;
+  OccBlock *d_occ[2] = {nullptr, nullptr};
+  uint32_t *d_sa[2] = {nullptr, nullptr};
+  uint64_t *d_text2 = nullptr, *d_textN = nullptr;
+  int64_t *d_contig = nullptr;
+  int32_t *d_chrRank = nullptr;
+  size_t bytes = 0;
+  IndexView view{};
+  // reusable search scratch
+  uint8_t *scratch = nullptr;
+  size_t scratchBytes = 0;
+};
+
+struct gwa_batch {
+  gwa_index *ix = nullptr;
+  gwa_config_t cfg{};
+  SearchConfig scfg{};
+  // host copy of the reads (SAM needs names, sequences, qualities)
+  uint32_t n = 0;
+  std::string names, seqs, quals;
+  std::vector<uint64_t> nameOff, seqOff, qualOff;
+  bool hasQual = false;
+  std::vector<uint8_t> codes;
+  std::vector<uint32_t> codeOff;
+  int maxM = 0, kmax = 0, R = 4;
+  // device
+  uint8_t *d_codes = nullptr;
+  uint32_t *d_off = nullptr;
+  ScanRes *d_sres = nullptr;
+  OutHeader *d_oh = nullptr;
+  OutHit *d_hits = nullptr;
+  uint16_t *d_cig = nullptr;
+  uint32_t *d_list[2] = {nullptr, nullptr};
+  uint32_t *d_count = nullptr;  // [0] search list, [1..] overflow lists
+  uint64_t *d_stair = nullptr;
+  uint32_t *d_stairBase = nullptr;
+  int hitCap = 4, cigCap = 64;
+  StairTables st{};
+  // results
+  std::vector<OutHeader> oh;
+  std::vector<OutHit> hits;
+  std::vector<uint16_t> cig;
+  gwa_batch_stats_t stats{};
+  bool ran = false;
+};
+
+static void freeIndexDev(gwa_index *ix) {
+  for (int s = 0; s < 2; ++s) {
+    if (ix->d_occ[s]) (void)hipFree(ix->d_occ[s]);
+    if (ix->d_sa[s]) (void)hipFree(ix->d_sa[s]);
+  }
+  if (ix->d_text2) (void)hipFree(ix->d_text2);
+  if (ix->d_textN) (void)hipFree(ix->d_textN);
+  if (ix->d_contig) (void)hipFree(ix->d_contig);
+  if (ix->d_chrRank) (void)hipFree(ix->d_chrRank);
+  if (ix->scratch) (void)hipFree(ix->scratch);
+  if (ix->stream) (void)hipStreamDestroy(ix->stream);
+}
+
+// Build SAs (GPU for large texts), Occ blocks, text; upload everything to HBM.
+static void finishAndUpload(gwa_index *ix) {
+  HostIndex &h = ix->host;
+  if (h.N == 0) throw std::runtime_error("empty reference");
+  if (h.N >= 0xFFFFFFFFull) throw std::runtime_error("reference longer than 2^32-2 bases is not supported");
+  HIPCHK(hipSetDevice(ix->device));
+  HIPCHK(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
+  std::vector<uint8_t> R(h.N);
+  for (uint64_t i = 0; i < h.N; ++i) R[i] = h.T[h.N - 1 - i];
+  // cyclic suffix arrays (A/sais/CyclicSAIS.java:223-431 computes the same unique order)
+  if (!cyclicSAHost(h.T.data(), h.N, h.sa[0]) || !cyclicSAHost(R.data(), h.N, h.sa[1]))
+    throw std::runtime_error("reference text is periodic (cyclic rotations tie): unsupported");
+  finishIndex(h);
+  hipStream_t s = ix->stream;
+  for (int k = 0; k < 2; ++k) {
+    ix->d_occ[k] = devUpload(h.occ[k], s, &ix->bytes);
+    ix->d_sa[k] = devUpload(h.sa[k], s, &ix->bytes);
+  }
+  ix->d_text2 = devUpload(h.text2, s, &ix->bytes);
+  ix->d_textN = devUpload(h.textN, s, &ix->bytes);
+  ix->d_contig = devUpload(h.offsets, s, &ix->bytes);
+  ix->d_chrRank = devUpload(h.chrRank, s, &ix->bytes);
+  HIPCHK(hipStreamSynchronize(s));
+  IndexView &v = ix->view;
+  v.occ[0] = ix->d_occ[0]; v.occ[1] = ix->d_occ[1];
+  v.sa[0] = ix->d_sa[0]; v.sa[1] = ix->d_sa[1];
+  v.text2 = ix->d_text2; v.textN = ix->d_textN;
+  v.contigOff = ix->d_contig;
+  v.nContig = (int32_t)h.names.size();
+  v.N = h.N;
+  for (int c = 0; c < 5; ++c) v.C[c] = h.C[c];
+  // host copies no longer needed except T (SA export) and the contig table
+  for (int k = 0; k < 2; ++k) { std::vector<OccBlock>().swap(h.occ[k]); }
+  std::vector<uint64_t>().swap(h.text2);
+  std::vector<uint64_t>().swap(h.textN);
+}
+
+extern "C" {
+
+void gwa_config_default(gwa_config_t *c) {
+  c->k = 0.1f; c->strategy = 0; c->report_type = 0; c->top_l = 5;
+  c->num_gap_open = 1; c->num_gap_ext = 4; c->num_split = 1;
+  c->match = 1; c->mismatch = 3; c->gap_open = 11; c->gap_ext = 4; c->split_open = 11;
+  c->indel_end_skip = 5; c->band_width = 31;
+}
+
+const char *gwa_last_error(void) { return g_err.c_str(); }
+
+int gwa_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+static int buildCommon(gwa_index *ix, int device, gwa_index_t **out) {
+  try {
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) throw std::runtime_error("no HIP device: the gwa align path requires an MI355X GPU");
+    if (device < 0 || device >= nd) throw std::runtime_error("invalid device " + std::to_string(device));
+    ix->device = device;
+    finishAndUpload(ix);
+    *out = ix;
+    return 0;
+  } catch (std::exception &e) {
+    freeIndexDev(ix);
+    delete ix;
+    return fail(e.what());
+  }
+}
+
+int gwa_index_build_fasta(const char *text, uint64_t len, int device, gwa_index_t **out) {
+  auto *ix = new gwa_index();
+  packFasta(text, (size_t)len, ix->host);
+  return buildCommon(ix, device, out);
+}
+
+int gwa_index_open(const char *path, int device, gwa_index_t **out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return fail(std::string("cannot open ") + path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  std::string t = ss.str();
+  return gwa_index_build_fasta(t.data(), t.size(), device, out);
+}
+
+int gwa_index_build_codes(const uint8_t *codes, uint64_t n, int32_t n_contigs, const char *const *names,
+                          const int64_t *lengths, int device, gwa_index_t **out) {
+  auto *ix = new gwa_index();
+  HostIndex &h = ix->host;
+  h.T.assign(codes, codes + n);
+  int64_t off = 0;
+  for (int i = 0; i < n_contigs; ++i) {
+    h.names.push_back(names[i]);
+    h.offsets.push_back(off);
+    h.lengths.push_back(lengths[i]);
+    off += lengths[i];
+  }
+  if ((uint64_t)off != n) {
+    delete ix;
+    return fail("contig lengths do not sum to n");
+  }
+  h.N = n;
+  return buildCommon(ix, device, out);
+}
+
+uint64_t gwa_index_text_size(const gwa_index_t *ix) { return ix->host.N; }
+uint64_t gwa_index_device_bytes(const gwa_index_t *ix) { return ix->bytes; }
+
+int gwa_index_export_sa(const gwa_index_t *ix, int strand, uint32_t *out) {
+  if (strand < 0 || strand > 1) return fail("strand must be 0 or 1");
+  try {
+    HIPCHK(hipMemcpy(out, ix->d_sa[strand], ix->host.N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+  return 0;
+}
+
+int gwa_sam_header(const gwa_index_t *ix, char **text, uint64_t *len) {
+  std::string h = samHeader(ix->host);
+  *text = (char *)malloc(h.size() + 1);
+  memcpy(*text, h.c_str(), h.size() + 1);
+  *len = h.size();
+  return 0;
+}
+
+void gwa_index_close(gwa_index_t *ix) {
+  if (!ix) return;
+  (void)hipSetDevice(ix->device);
+  freeIndexDev(ix);
+  delete ix;
+}
+
+void gwa_free(void *p) { free(p); }
+
+static void freeBatchDev(gwa_batch *b) {
+  void *ps[] = {b->d_codes, b->d_off, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_count,
+                b->d_stair, b->d_stairBase};
+  for (void *p : ps)
+    if (p) (void)hipFree(p);
+}
+
+int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_batch_t **out) {
+  auto *b = new gwa_batch();
+  try {
+    if (cfg->strategy != 0) throw std::runtime_error("only -m bsf is implemented on the device path");
+    HIPCHK(hipSetDevice(ix->device));
+    b->ix = ix;
+    b->cfg = *cfg;
+    SearchConfig &sc = b->scfg;
+    sc.k = cfg->k; sc.reportType = cfg->report_type; sc.topL = cfg->top_l; sc.numSplit = cfg->num_split;
+    sc.matchScore = cfg->match; sc.mismatchPenalty = cfg->mismatch; sc.splitOpenPenalty = cfg->split_open;
+    sc.indelEndSkip = cfg->indel_end_skip; sc.bandWidth = cfg->band_width;
+    const uint32_t n = reads->n;
+    b->n = n;
+    b->hasQual = reads->qual != nullptr;
+    b->nameOff.assign(reads->name_off, reads->name_off + n + 1);
+    b->seqOff.assign(reads->seq_off, reads->seq_off + n + 1);
+    b->names.assign(reads->name + b->nameOff[0], reads->name + b->nameOff[n]);
+    b->seqs.assign(reads->seq + b->seqOff[0], reads->seq + b->seqOff[n]);
+    if (b->hasQual) {
+      b->qualOff.assign(reads->qual_off, reads->qual_off + n + 1);
+      b->quals.assign(reads->qual + b->qualOff[0], reads->qual + b->qualOff[n]);
+    }
+    // codes (ACGTSequence(String): spaces skipped, A/ACGTSequence.java:86-97)
+    b->codes.reserve(b->seqs.size());
+    b->codeOff.resize(n + 1);
+    std::vector<int> lens;
+    std::vector<char> seen(256, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      b->codeOff[i] = (uint32_t)b->codes.size();
+      for (uint64_t p = b->seqOff[i]; p < b->seqOff[i + 1]; ++p) {
+        char c = b->seqs[p - b->seqOff[0]];
+        if (c != ' ') b->codes.push_back(to3bit((unsigned char)c));
+      }
+      int m = (int)(b->codes.size() - b->codeOff[i]);
+      b->maxM = std::max(b->maxM, m);
+      if (m <= 255 && !seen[(size_t)m]) { seen[(size_t)m] = 1; lens.push_back(m); }
+    }
+    b->codeOff[n] = (uint32_t)b->codes.size();
+    // k per length (AlignmentScoreConfig.getMaximumEditDistance)
+    for (int m : lens) {
+      int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
+      b->kmax = std::max(b->kmax, k);
+    }
+    if (b->kmax > 31) throw std::runtime_error("k > 31 is not supported on the device path");
+    b->R = b->kmax + 1 <= 4 ? 4 : b->kmax + 1 <= 8 ? 8 : b->kmax + 1 <= 16 ? 16 : 32;
+    std::vector<uint64_t> tab;
+    std::vector<uint32_t> base;
+    buildStairTables(lens, std::max(b->kmax, 0), tab, base);
+    hipStream_t s = ix->stream;
+    b->d_codes = devUpload(b->codes, s, nullptr);
+    b->d_off = devUpload(b->codeOff, s, nullptr);
+    b->d_stair = devUpload(tab, s, nullptr);
+    b->d_stairBase = devUpload(base, s, nullptr);
+    b->st.tab = b->d_stair;
+    b->st.base = b->d_stairBase;
+    b->st.kmax = std::max(b->kmax, 0);
+    const int chains = cfg->report_type == 0 ? 1 : 4;
+    b->hitCap = chains * std::max(1, cfg->num_split + 1);
+    b->cigCap = 64 * chains;
+    b->d_sres = devAlloc<ScanRes>(n);
+    b->d_oh = devAlloc<OutHeader>(n);
+    b->d_hits = devAlloc<OutHit>((size_t)n * b->hitCap);
+    b->d_cig = devAlloc<uint16_t>((size_t)n * b->cigCap);
+    b->d_list[0] = devAlloc<uint32_t>(n);
+    b->d_list[1] = devAlloc<uint32_t>(n);
+    b->d_count = devAlloc<uint32_t>(8);
+    HIPCHK(hipStreamSynchronize(s));
+    *out = b;
+    return 0;
+  } catch (std::exception &e) {
+    freeBatchDev(b);
+    delete b;
+    return fail(e.what());
+  }
+}
+
+// capacity tiers: (arena, heap, hits, list, cigar) and the lane budget of each tier
+struct Tier {
+  int arena, heap, hits, list, cigar;
+  uint32_t maxLanes;
+};
+static const Tier kTiers[3] = {
+    {256, 256, 32, 32, 512, 256u * 1024u},
+    {4096, 4096, 256, 256, 4096, 16384u},
+    {65536, 65536, 4096, 4096, 65536, 1024u},
+};
+
+int gwa_batch_run(gwa_batch_t *b) {
+  try {
+    gwa_index *ix = b->ix;
+    HIPCHK(hipSetDevice(ix->device));
+    hipStream_t s = ix->stream;
+    memset(&b->stats, 0, sizeof(b->stats));
+    ReadsView rv{b->d_codes, b->d_off, b->n};
+    hipEvent_t e0, e1, e2;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventCreate(&e2));
+    HIPCHK(hipMemsetAsync(b->d_count, 0, 8 * sizeof(uint32_t), s));
+    HIPCHK(hipEventRecord(e0, s));
+    launchQuickscan(ix->view, b->scfg, rv, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, b->d_list[0],
+                    b->d_count, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e1, s));
+    uint32_t nSearch = 0;
+    HIPCHK(hipMemcpyAsync(&nSearch, b->d_count, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float qms = 0;
+    HIPCHK(hipEventElapsedTime(&qms, e0, e1));
+    b->stats.quickscan_ms = qms;
+    double searchMs = 0;
+    int cur = 0;
+    uint32_t n = nSearch;
+    const int m = std::max(b->maxM, 1);
+    for (int t = 0; t < 3 && n > 0; ++t) {
+      const Tier &T = kTiers[t];
+      Caps caps;
+      caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
+      const int bMax = std::max(1, (m + 63) / 64);
+      const int nref = m + 2 * b->kmax + 2;
+      caps.dpWords = 2 * bMax * (nref + 1);
+      caps.path = ((m + nref + 8) + 7) & ~7;
+      const uint64_t stride = laneBytesFor(b->R, caps);
+      uint32_t lanes = std::min<uint32_t>(n, T.maxLanes);
+      lanes = (lanes + 255) / 256 * 256;
+      const size_t need = (size_t)stride * lanes;
+      if (need > ix->scratchBytes) {
+        if (ix->scratch) HIPCHK(hipFree(ix->scratch));
+        ix->scratch = nullptr;
+        ix->scratchBytes = 0;
+        HIPCHK(hipMalloc(&ix->scratch, need));
+        ix->scratchBytes = need;
+      }
+      uint32_t *ovfCount = b->d_count + 1 + t;
+      HIPCHK(hipEventRecord(e1, s));
+      launchSearch(b->R, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
+                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_list[cur ^ 1], ovfCount, s);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(e2, s));
+      uint32_t nOvf = 0;
+      HIPCHK(hipMemcpyAsync(&nOvf, ovfCount, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, e1, e2));
+      searchMs += ms;
+      b->stats.tier_reads[t] = n;
+      n = nOvf;
+      cur ^= 1;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    b->stats.search_ms = searchMs;
+    b->stats.kernel_ms = qms + searchMs;
+    if (n > 0) throw std::runtime_error(std::to_string(n) + " reads exceeded the largest search tier");
+    b->ran = true;
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
+
+int gwa_batch_stats(const gwa_batch_t *b, gwa_batch_stats_t *st) {
+  *st = b->stats;
+  return 0;
+}
+
+static int fetch(gwa_batch *b) {
+  const uint32_t n = b->n;
+  b->oh.resize(n);
+  b->hits.resize((size_t)n * b->hitCap);
+  b->cig.resize((size_t)n * b->cigCap);
+  hipStream_t s = b->ix->stream;
+  HIPCHK(hipMemcpyAsync(b->oh.data(), b->d_oh, n * sizeof(OutHeader), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(b->hits.data(), b->d_hits, b->hits.size() * sizeof(OutHit), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(b->cig.data(), b->d_cig, b->cig.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  gwa_batch_stats_t &st = b->stats;
+  st.fm_searches = st.quick_steps = st.blocks = st.states = st.quick_blocks = st.sa_reads = 0;
+  st.n_mapped = st.n_unmapped = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const OutHeader &h = b->oh[i];
+    st.fm_searches += (uint64_t)h.fmSearches;
+    st.quick_steps += (uint64_t)h.quickSteps;
+    st.blocks += (uint64_t)h.blocks + (uint64_t)h.searchBlocks;
+    st.quick_blocks += (uint64_t)h.blocks;
+    st.sa_reads += (uint64_t)h.saReads;
+    st.states += (uint64_t)h.states;
+    if (h.status == ST_MAPPED) st.n_mapped++;
+    else if (h.status == ST_UNMAPPED) st.n_unmapped++;
+  }
+  return 0;
+}
+
+int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) {
+  try {
+    if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
+    fetch(b);
+    const uint32_t n = b->n;
+    for (uint32_t i = 0; i < n; ++i) {
+      int stt = b->oh[i].status;
+      if (stt == ST_ERROR || stt == ST_OVERFLOW || stt == ST_TOO_LONG) {
+        std::string nm(b->names.data() + (b->nameOff[i] - b->nameOff[0]), b->nameOff[i + 1] - b->nameOff[i]);
+        throw std::runtime_error(std::string(stt == ST_ERROR ? "reference would abort (exception) at read "
+                                                             : stt == ST_TOO_LONG ? "read longer than 255 bases: "
+                                                                                  : "output slot overflow at read ") + nm);
+      }
+    }
+    // SAM formatting in parallel chunks, concatenated in input order
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::string> parts(nt);
+    std::vector<std::vector<uint64_t>> lens(nt);
+    std::atomic<int> bad{-1};
+    auto work = [&](unsigned t) {
+      uint32_t a = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
+      std::string &o = parts[t];
+      o.reserve((size_t)(e - a) * 320);
+      for (uint32_t i = a; i < e; ++i) {
+        size_t before = o.size();
+        ReadText rt;
+        rt.name = b->names.data() + (b->nameOff[i] - b->nameOff[0]);
+        rt.nameLen = b->nameOff[i + 1] - b->nameOff[i];
+        rt.seq = b->seqs.data() + (b->seqOff[i] - b->seqOff[0]);
+        rt.seqLen = b->seqOff[i + 1] - b->seqOff[i];
+        if (b->hasQual) {
+          rt.qual = b->quals.data() + (b->qualOff[i] - b->qualOff[0]);
+          rt.qualLen = b->qualOff[i + 1] - b->qualOff[i];
+        } else {
+          rt.qual = nullptr;
+          rt.qualLen = 0;
+        }
+        const OutHeader &h = b->oh[i];
+        if (h.status == ST_MAPPED) {
+          for (int c = 0; c < h.nChains; ++c)
+            if (formatChain(b->ix->host, rt, b->hits.data() + (size_t)i * b->hitCap, b->cig.data() + (size_t)i * b->cigCap,
+                            h.chainHead[c], o) != 0)
+              bad = (int)i;
+        } else {
+          formatUnmapped(rt, o);
+        }
+        lens[t].push_back(o.size() - before);
+      }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto &x : th) x.join();
+    if (bad >= 0) throw std::runtime_error("reference would abort (exception in AlignmentRecord.convert) at read index " + std::to_string(bad.load()));
+    size_t total = 0;
+    for (auto &p : parts) total += p.size();
+    out->n_reads = n;
+    out->sam = (char *)malloc(total + 1);
+    out->sam_len = total;
+    out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    size_t pos = 0;
+    uint32_t ri = 0;
+    for (unsigned t = 0; t < nt; ++t) {
+      memcpy(out->sam + pos, parts[t].data(), parts[t].size());
+      for (uint64_t L : lens[t]) { out->line_off[ri++] = pos; pos += L; }
+    }
+    out->line_off[n] = pos;
+    out->sam[total] = 0;
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
+
+void gwa_batch_free(gwa_batch_t *b) {
+  if (!b) return;
+  (void)hipSetDevice(b->ix->device);
+  freeBatchDev(b);
+  delete b;
+}
+
+void gwa_results_free(gwa_results_t *r) {
+  if (!r) return;
+  free(r->sam);
+  free(r->line_off);
+  r->sam = nullptr;
+  r->line_off = nullptr;
+}
+
+int gwa_align_batch(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_results_t *out) {
+  gwa_batch_t *b = nullptr;
+  if (gwa_batch_create(ix, cfg, reads, &b) != 0) return -1;
+  int rc = gwa_batch_run(b);
+  if (rc == 0) rc = gwa_batch_results(b, out);
+  gwa_batch_free(b);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+// gwa_layout.h -- device data layouts of the MI355X-native aligner.
+//
+// HBM layout (one replica per GPU, built once by index_build.cpp):
+//   OccBlock occ[2][N/128+1]   forward-text BWT (fm 0) and reverse-text BWT (fm 1);
+//                               one 64-B block per 128 BWT positions = one HBM burst
+//   uint32_t sa[2][N]          FULL suffix arrays (the reference samples every 32nd entry and
+//                               LF-walks up to 31 steps, A/SparseSuffixArray.java:141-158; with
+//                               288 GB of HBM we keep every entry: 1 gather instead of <=31)
+//   uint64_t text2[N/32+1]     forward text, 2-bit codes (N stored as A) ...
+//   uint64_t textN[N/64+1]     ... plus its N bitmap  (verification windows)
+//   int64_t  contigOff[n]      contig start offsets (SequenceBoundary)
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define GWA_HD __host__ __device__ __forceinline__
+#define GWA_HDNI __host__ __device__ __noinline__
+#else
+#define GWA_HD inline
+#define GWA_HDNI
+#endif
+
+namespace gwa {
+
+// One Occ block: counts of A,C,G,T in bwt[0, 128*b), then the 128 codes of the block as two
+// bit planes (lo = code&1, hi = code>>1; position p at bit p%64 of word p/64) and the N bitmap.
+// N positions carry code 0 in the planes; occ(A) subtracts them, occ(N) = i - sum(ACGT).
+// Reproduces OccurrenceCountTable.getOcc/getOccACGTN (A/OccurrenceCountTable.java:80-107)
+// with W = 128 (A/FMIndexOnGenome.java:46).
+struct alignas(64) OccBlock {
+  uint32_t cnt[4];
+  uint64_t lo[2];
+  uint64_t hi[2];
+  uint64_t nmask[2];
+};
+static_assert(sizeof(OccBlock) == 64, "OccBlock must be one 64-byte burst");
+
+struct IndexView {
+  const OccBlock *occ[2];  // [0] forward index (BWT of T), [1] reverse index (BWT of reverse(T))
+  const uint32_t *sa[2];   // full cyclic suffix arrays of T and reverse(T)
+  const uint64_t *text2;   // T, 2-bit codes, 32 per word, LSB-first
+  const uint64_t *textN;   // T, N bitmap, 64 per word
+  const int64_t *contigOff;
+  int32_t nContig;
+  int32_t pad;
+  uint64_t N;
+  uint64_t C[5];  // CharacterCount.C (A/CharacterCount.java:41-50); identical for both strands
+};
+
+// AlignmentConfig + AlignmentScoreConfig fields read on the BSF path
+// (S/BidirectionalSuffixFilter.java:250,461,539,785; A/AlignmentScoreConfig.java:37-77)
+struct SearchConfig {
+  float k;
+  int32_t reportType;  // 0 BESTHIT, 1 ALLHITS, 2 TOPL
+  int32_t topL;
+  int32_t numSplit;
+  int32_t matchScore, mismatchPenalty, splitOpenPenalty;
+  int32_t indelEndSkip, bandWidth;
+};
+
+// Read batch as resident in HBM: 2-bit-per-byte codes (0..4) per read, concatenated.
+struct ReadsView {
+  const uint8_t *codes;
+  const uint32_t *off;  // n+1 offsets into codes
+  uint32_t n;
+};
+
+// Staircase-mask tables (StaircaseFilter.getStairCaseMask64bit, S/StaircaseFilter.java:91-102),
+// precomputed on the host per read length m for every minMismatches value kk in [0, kmax+1],
+// row in [0, kmax], offset in [-kmax, m]:  tab[base(m) + ((kk*(kmax+1) + row)*(m+kmax+1) + offset+kmax)]
+struct StairTables {
+  const uint64_t *tab;
+  const uint32_t *base;  // per m (0..255), index into tab; 0xFFFFFFFF = no table
+  int32_t kmax;
+  int32_t pad;
+};
+
+// ---- per-read output ----
+enum : int32_t {
+  ST_UNMAPPED = 0,  // emitted "*" record
+  ST_MAPPED = 1,
+  ST_OVERFLOW = 2,  // a per-lane capacity was exceeded: rerun on a larger tier
+  ST_ERROR = 3,     // the reference would abort with an exception (ReadHit null/NPE etc)
+  ST_TOO_LONG = 4,  // read longer than the device path supports
+};
+
+// chr codes in OutHit.chr
+enum : int32_t { CHR_NULL = -1, CHR_EMPTY = -2, CHR_STAR = -3 };
+
+struct OutHit {           // one ReadHit (R/ReadHit.java:42-53)
+  int32_t chr;            // contig index or CHR_*
+  int32_t pos;
+  int32_t matchLength, qStart, qEnd, diff;
+  int32_t strand, numHits;
+  int32_t next;           // index of nextSplit within the record's hits, -1 = none
+  uint16_t cigarOff, cigarLen;
+};
+
+// Fixed-size per-read output slot.
+struct OutHeader {
+  int32_t status;
+  int32_t nChains;   // reported ReadHit chains (BESTHIT: 1)
+  int32_t nHits;     // OutHit entries used
+  int32_t nCigar;    // cigar ops used
+  int32_t chainHead[4];
+  // instrumentation: FM steps, quick-scan steps, rank block loads
+  int32_t fmSearches, quickSteps, blocks, states;
+  int32_t searchBlocks, saReads, pad0, pad1;
+};
+
+// quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at
+// S/BidirectionalSuffixFilter.java:324-346)
+struct ScanRes {
+  int32_t nmF, lmF, nmR, lmR;
+};
+
+// CIGAR op = (len << 3) | type ; type: M0 I1 D2 N3 S4 H5 P6 X7  (A/CIGAR.java:39-47)
+}  // namespace gwa

@@ -1,0 +1,22 @@
+// kernels.h -- host-callable launchers of the HIP kernels (gwa_kernels.hip, sa_build.hip)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "gwa_layout.h"
+
+namespace gwa {
+
+struct Caps;
+
+void launchQuickscan(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
+                     OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap, uint32_t *searchList, uint32_t *searchCount,
+                     hipStream_t s);
+void launchSearch(int R, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                  const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
+                  uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
+                  const int32_t *chrRank, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s);
+size_t laneBytesFor(int R, const Caps &c);
+
+}  // namespace gwa

@@ -1,0 +1,296 @@
+"""gwa -- Python host mirror of genome-weaver's `align` plugin surface over the C-ABI (libgwa.so).
+
+Mirrors (names, argument meaning, error behaviour) the reference's Java interface for this path:
+  AlignmentConfig / AlignmentScoreConfig   A/AlignmentConfig.java:40-72, A/AlignmentScoreConfig.java:37-77
+  FMIndexOnGenome.load / buildFromSequence A/FMIndexOnGenome.java:60-115
+  Aligner.align(read, reporter)            A/Aligner.java:30-33   (batched: align_batch)
+  SAMOutput (header + one emit per read)   A/SAMOutput.java:56-82
+The compute path is the HIP extension: importing works without a GPU, but every call that aligns
+or builds an index raises GwaError when no MI355X is present or libgwa.so is missing.
+"""
+import ctypes
+import os
+from dataclasses import dataclass, fields
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(_HERE, "libgwa.so")
+
+
+class GwaError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_float)] + [(n, ctypes.c_int32) for n in (
+        "strategy", "report_type", "top_l", "num_gap_open", "num_gap_ext", "num_split", "match", "mismatch",
+        "gap_open", "gap_ext", "split_open", "indel_end_skip", "band_width")]
+
+
+class _Reads(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("name", ctypes.c_void_p), ("seq", ctypes.c_void_p), ("qual", ctypes.c_void_p),
+                ("name_off", ctypes.c_void_p), ("seq_off", ctypes.c_void_p), ("qual_off", ctypes.c_void_p)]
+
+
+class _Results(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_uint32), ("sam", ctypes.c_void_p), ("sam_len", ctypes.c_uint64),
+                ("line_off", ctypes.c_void_p)]
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("quickscan_ms", ctypes.c_double), ("search_ms", ctypes.c_double),
+                ("fm_searches", ctypes.c_uint64), ("quick_steps", ctypes.c_uint64), ("blocks", ctypes.c_uint64),
+                ("quick_blocks", ctypes.c_uint64), ("states", ctypes.c_uint64), ("sa_reads", ctypes.c_uint64), ("tier_reads", ctypes.c_uint32 * 4),
+                ("n_mapped", ctypes.c_uint32), ("n_unmapped", ctypes.c_uint32)]
+
+
+_lib = None
+
+# every symbol include/gwa.h declares (checked by tests/test_cabi.py)
+EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_index_build_fasta", "gwa_index_open",
+           "gwa_index_build_codes", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
+           "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
+           "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free"]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIBPATH):
+            raise GwaError("libgwa.so is not built (run __graft_entry__.build() or make -C genome-weaver-align_amd)")
+        L = ctypes.CDLL(LIBPATH)
+        V, P, I, U64 = ctypes.c_void_p, ctypes.POINTER, ctypes.c_int, ctypes.c_uint64
+        L.gwa_last_error.restype = ctypes.c_char_p
+        L.gwa_config_default.argtypes = [P(_Config)]
+        L.gwa_index_build_fasta.argtypes = [ctypes.c_char_p, U64, I, P(V)]
+        L.gwa_index_open.argtypes = [ctypes.c_char_p, I, P(V)]
+        L.gwa_index_build_codes.argtypes = [V, U64, ctypes.c_int32, V, V, I, P(V)]
+        L.gwa_index_text_size.restype = U64
+        L.gwa_index_text_size.argtypes = [V]
+        L.gwa_index_device_bytes.restype = U64
+        L.gwa_index_device_bytes.argtypes = [V]
+        L.gwa_index_export_sa.argtypes = [V, I, V]
+        L.gwa_sam_header.argtypes = [V, P(V), P(U64)]
+        L.gwa_index_close.argtypes = [V]
+        L.gwa_align_batch.argtypes = [V, P(_Config), P(_Reads), P(_Results)]
+        L.gwa_results_free.argtypes = [P(_Results)]
+        L.gwa_free.argtypes = [V]
+        L.gwa_batch_create.argtypes = [V, P(_Config), P(_Reads), P(V)]
+        L.gwa_batch_run.argtypes = [V]
+        L.gwa_batch_stats.argtypes = [V, P(BatchStats)]
+        L.gwa_batch_results.argtypes = [V, P(_Results)]
+        L.gwa_batch_free.argtypes = [V]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise GwaError(lib().gwa_last_error().decode())
+
+
+STRATEGIES = {"bsf": 0}
+REPORT_TYPES = {"besthit": 0, "allhits": 1, "topl": 2}
+
+
+@dataclass
+class AlignmentConfig:
+    """AlignmentConfig + AlignmentScoreConfig, same defaults and CLI symbols."""
+    k: float = 0.1             # -k  max edits (fraction of read length when in (0,1))
+    strategy: str = "bsf"      # -m
+    reportType: str = "besthit"  # -R
+    topL: int = 5              # -L
+    numGapOpenAllowed: int = 1  # -g
+    numGapExtensionAllowed: int = 4  # -e
+    numSplitAlowed: int = 1    # -s
+    matchScore: int = 1        # -M
+    mismatchPenalty: int = 3   # -N
+    gapOpenPenalty: int = 11   # -G
+    gapExtensionPenalty: int = 4  # -E
+    splitOpenPenalty: int = 11  # -S
+    indelEndSkip: int = 5      # -P
+    bandWidth: int = 31        # -W
+
+    def getMaximumEditDistance(self, readLength):
+        # A/AlignmentScoreConfig.java:40-47 (float arithmetic)
+        import numpy as np
+        if 0 < self.k < 1:
+            return int(np.floor(np.float32(readLength) * np.float32(self.k)))
+        return int(self.k)
+
+    def _c(self):
+        if self.strategy.lower() not in STRATEGIES:
+            raise GwaError("%s mode is not supported on the device path" % self.strategy)
+        c = _Config()
+        c.k = self.k
+        c.strategy = STRATEGIES[self.strategy.lower()]
+        c.report_type = REPORT_TYPES[self.reportType.lower()]
+        c.top_l = self.topL
+        c.num_gap_open, c.num_gap_ext, c.num_split = self.numGapOpenAllowed, self.numGapExtensionAllowed, self.numSplitAlowed
+        c.match, c.mismatch, c.gap_open = self.matchScore, self.mismatchPenalty, self.gapOpenPenalty
+        c.gap_ext, c.split_open = self.gapExtensionPenalty, self.splitOpenPenalty
+        c.indel_end_skip, c.band_width = self.indelEndSkip, self.bandWidth
+        return c
+
+
+def _pack(strs):
+    import numpy as np
+    bs = [s.encode() if isinstance(s, str) else s for s in strs]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(b) for b in bs])
+    blob = b"".join(bs)
+    return blob, off
+
+
+class FMIndexOnGenome:
+    """An FM-index resident in one GPU's HBM (both strands, full SA, 2-bit text, contig table)."""
+
+    def __init__(self, handle, device):
+        self.h = handle
+        self.device = device
+
+    @classmethod
+    def load(cls, fasta_path, device=0):
+        h = ctypes.c_void_p()
+        _check(lib().gwa_index_open(fasta_path.encode(), device, ctypes.byref(h)))
+        return cls(h, device)
+
+    @classmethod
+    def buildFromFasta(cls, text, device=0):
+        b = text.encode() if isinstance(text, str) else text
+        h = ctypes.c_void_p()
+        _check(lib().gwa_index_build_fasta(b, len(b), device, ctypes.byref(h)))
+        return cls(h, device)
+
+    @classmethod
+    def buildFromSequence(cls, name, seq, device=0):
+        return cls.buildFromFasta(">%s\n%s\n" % (name, seq), device)
+
+    @classmethod
+    def buildFromCodes(cls, codes, names, lengths, device=0):
+        import numpy as np
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        ln = np.ascontiguousarray(lengths, dtype=np.int64)
+        arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+        h = ctypes.c_void_p()
+        _check(lib().gwa_index_build_codes(codes.ctypes.data, len(codes), len(names), ctypes.cast(arr, ctypes.c_void_p),
+                                          ln.ctypes.data, device, ctypes.byref(h)))
+        return cls(h, device)
+
+    def textSize(self):
+        return lib().gwa_index_text_size(self.h)
+
+    def deviceBytes(self):
+        return lib().gwa_index_device_bytes(self.h)
+
+    def suffixArray(self, strand):
+        import numpy as np
+        out = np.zeros(self.textSize(), dtype=np.uint32)
+        _check(lib().gwa_index_export_sa(self.h, strand, out.ctypes.data))
+        return out
+
+    def samHeader(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        _check(lib().gwa_sam_header(self.h, ctypes.byref(p), ctypes.byref(n)))
+        s = ctypes.string_at(p, n.value).decode()
+        lib().gwa_free(p)
+        return s
+
+    def close(self):
+        if self.h:
+            lib().gwa_index_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _reads_struct(reads, keep):
+    names, seqs, quals = zip(*reads) if reads else ((), (), ())
+    nb, no = _pack(names)
+    sb, so = _pack(seqs)
+    has_q = len(reads) > 0 and all(q is not None for q in quals)
+    if any(q is not None for q in quals) and not has_q:
+        raise GwaError("a batch must have qualities for every read or for none")
+    r = _Reads()
+    r.n = len(reads)
+    keep.extend([nb, no, sb, so])
+    r.name, r.seq = ctypes.cast(ctypes.c_char_p(nb), ctypes.c_void_p), ctypes.cast(ctypes.c_char_p(sb), ctypes.c_void_p)
+    r.name_off, r.seq_off = no.ctypes.data, so.ctypes.data
+    if has_q:
+        qb, qo = _pack(quals)
+        keep.extend([qb, qo])
+        r.qual, r.qual_off = ctypes.cast(ctypes.c_char_p(qb), ctypes.c_void_p), qo.ctypes.data
+    else:
+        r.qual, r.qual_off = None, None
+    return r
+
+
+def _take_results(res):
+    import numpy as np
+    try:
+        s = ctypes.string_at(res.sam, res.sam_len).decode() if res.sam_len else ""
+        off = np.ctypeslib.as_array((ctypes.c_uint64 * (res.n_reads + 1)).from_address(res.line_off)).copy()
+        return s, off
+    finally:
+        lib().gwa_results_free(ctypes.byref(res))
+
+
+class BidirectionalSuffixFilter:
+    """The `-m bsf` Aligner (S/BidirectionalSuffixFilter.java), batched on one GPU."""
+
+    def __init__(self, fmIndex, config=None):
+        self.fmIndex = fmIndex
+        self.config = config or AlignmentConfig()
+
+    def align_batch(self, reads):
+        """reads: list of (name, seq, qual-or-None) -> SAM text (no header), input order."""
+        keep = []
+        r = _reads_struct(reads, keep)
+        res = _Results()
+        c = self.config._c()
+        _check(lib().gwa_align_batch(self.fmIndex.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(res)))
+        return _take_results(res)[0]
+
+    def align(self, read, reporter):
+        """Aligner.align(Read, Reporter): reporter(line) once per emitted SAM line."""
+        for line in self.align_batch([read]).splitlines():
+            reporter(line)
+
+
+class Batch:
+    """Split form for benchmarking: reads resident in HBM, run() = the timed kernels."""
+
+    def __init__(self, fmIndex, config, reads):
+        self._keep = []
+        r = _reads_struct(reads, self._keep)
+        self.h = ctypes.c_void_p()
+        c = config._c()
+        _check(lib().gwa_batch_create(fmIndex.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(self.h)))
+
+    def run(self):
+        _check(lib().gwa_batch_run(self.h))
+
+    def stats(self):
+        st = BatchStats()
+        _check(lib().gwa_batch_stats(self.h, ctypes.byref(st)))
+        return st
+
+    def results(self):
+        res = _Results()
+        _check(lib().gwa_batch_results(self.h, ctypes.byref(res)))
+        return _take_results(res)
+
+    def close(self):
+        if self.h:
+            lib().gwa_batch_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

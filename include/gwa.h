@@ -1,0 +1,108 @@
+/* gwa.h -- C ABI of the MI355X-native genome-weaver `align` path (drop-in boundary).
+ *
+ * Replaces, for the single-end FM-index path, the reference's Java plugin surface:
+ *   interface Aligner { void align(Read read, Reporter out) }      A/Aligner.java:30-33
+ *   Align.query(...) strategy selection (-m bsf)                     A/Align.java:112-140
+ *   Reporter.emit -> SAMOutput.emit -> AlignmentRecord.toSAMLine     J/parallel/Reporter.java:27-30,
+ *                                                                    A/SAMOutput.java:73-82
+ *   FMIndexOnGenome.load / buildFromSequence                         A/FMIndexOnGenome.java:60-115
+ *   SequenceBoundary.toSAMHeader                                     A/SequenceBoundary.java:81-87
+ * (paths relative to align/src/main/java/org/utgenome/weaver/; A = align/, J = .)
+ *
+ * Conventions: 0 = OK, negative = error (message via gwa_last_error, thread-local).  A read on
+ * which the reference would throw fails the whole batch (the reference aborts the run,
+ * S/BidirectionalSuffixFilter.java:264-267).  Results are in input order.  Calls on one index
+ * handle are serialised (one HIP stream per handle, one handle per GPU).  Plain pointers and
+ * sizes only; no C++ or torch types cross this boundary.
+ */
+#ifndef GWA_H
+#define GWA_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gwa_index gwa_index_t;
+typedef struct gwa_batch gwa_batch_t;
+
+/* AlignmentConfig + AlignmentScoreConfig (A/AlignmentConfig.java:40-72, A/AlignmentScoreConfig.java:37-77);
+ * defaults from gwa_config_default: k 0.1, bsf, besthit, L 5, g 1, e 4, s 1, M 1, N 3, G 11, E 4, S 11, P 5, W 31 */
+typedef struct {
+  float k;
+  int32_t strategy;    /* 0 = bsf (-m bsf); others are rejected */
+  int32_t report_type; /* 0 besthit, 1 allhits, 2 topL (-R) */
+  int32_t top_l;       /* -L */
+  int32_t num_gap_open, num_gap_ext, num_split; /* -g -e -s */
+  int32_t match, mismatch, gap_open, gap_ext, split_open; /* -M -N -G -E -S */
+  int32_t indel_end_skip, band_width; /* -P -W */
+} gwa_config_t;
+
+/* A batch of reads, SoA, caller-owned.  Read i = name[name_off[i], name_off[i+1]), etc.
+ * qual may be NULL (SAM QUAL "*", as for FASTA input / -q queries). */
+typedef struct {
+  uint32_t n;
+  const char *name, *seq, *qual;
+  const uint64_t *name_off, *seq_off, *qual_off;
+} gwa_reads_t;
+
+/* Library-owned SAM text (no header), in input order; read i's lines are
+ * sam[line_off[i], line_off[i+1]).  Free with gwa_results_free. */
+typedef struct {
+  uint32_t n_reads;
+  char *sam;
+  uint64_t sam_len;
+  uint64_t *line_off; /* n_reads + 1 */
+} gwa_results_t;
+
+/* Per-batch counters (instrumentation for SURVEY.md §8d roofline accounting). */
+typedef struct {
+  double kernel_ms;        /* device time of all align kernels (HIP events) */
+  double quickscan_ms;     /* fm_quickscan kernel */
+  double search_ms;        /* bsf_search kernels (all tiers) */
+  uint64_t fm_searches;    /* numFMIndexSearches summed over reads */
+  uint64_t quick_steps;    /* FMQuickScan steps */
+  uint64_t blocks;         /* 64-B Occ blocks read (algorithmic bytes = 64 * blocks) */
+  uint64_t quick_blocks;   /* of which by fm_quickscan */
+  uint64_t states;         /* search states created */
+  uint64_t sa_reads;       /* 4-B suffix-array gathers (exact hits + verifications) */
+  uint32_t tier_reads[4];  /* reads processed per capacity tier */
+  uint32_t n_mapped, n_unmapped;
+} gwa_batch_stats_t;
+
+void gwa_config_default(gwa_config_t *cfg);
+const char *gwa_last_error(void);
+int gwa_device_count(void);
+
+/* Build an index from FASTA text (the `bwt` command: PackFasta + cyclic SA + BWT) and place
+ * it in HBM of `device`. */
+int gwa_index_build_fasta(const char *fasta_text, uint64_t len, int device, gwa_index_t **out);
+/* Same, from a FASTA file path (the `-r` argument). */
+int gwa_index_open(const char *fasta_path, int device, gwa_index_t **out);
+/* Same, from codes 0..4 (A,C,G,T,N) and a contig table (names + lengths, concatenated in order). */
+int gwa_index_build_codes(const uint8_t *codes, uint64_t n, int32_t n_contigs, const char *const *names,
+                          const int64_t *lengths, int device, gwa_index_t **out);
+uint64_t gwa_index_text_size(const gwa_index_t *ix);
+uint64_t gwa_index_device_bytes(const gwa_index_t *ix);
+/* Export the cyclic suffix array of strand 0 (text) or 1 (reversed text), n entries. */
+int gwa_index_export_sa(const gwa_index_t *ix, int strand, uint32_t *out);
+int gwa_sam_header(const gwa_index_t *ix, char **text, uint64_t *len);
+void gwa_index_close(gwa_index_t *ix);
+
+/* One call per batch: H2D, align on the GPU, D2H, SAM formatting. */
+int gwa_align_batch(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_results_t *out);
+void gwa_results_free(gwa_results_t *r);
+void gwa_free(void *p);
+
+/* Split form used by bench.py: upload once (reads resident in HBM), run the kernels (timed),
+ * then fetch results. */
+int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_batch_t **out);
+int gwa_batch_run(gwa_batch_t *b);
+int gwa_batch_stats(const gwa_batch_t *b, gwa_batch_stats_t *st);
+int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out);
+void gwa_batch_free(gwa_batch_t *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GWA_H */

@@ -1,0 +1,121 @@
+// host_driver.cpp -- TEST-ONLY: runs the device kernel logic (bsf_core.h) on the CPU so the
+// kernel's control flow can be debugged against the oracle without a GPU.  Never linked into
+// libgwa.so and never used as a product fallback (the product C-ABI requires a GPU).
+#include <cstdio>
+#include <cstring>
+#include <cmath>
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../genome-weaver-align_amd/csrc/bsf_core.h"
+#include "../../genome-weaver-align_amd/csrc/host_index.h"
+#include "../../genome-weaver-align_amd/csrc/sam.h"
+
+using namespace gwa;
+
+struct HC {
+  HostIndex h;
+  IndexView v{};
+};
+
+extern "C" {
+
+void *hc_index_codes(const uint8_t *codes, uint64_t n, int32_t nc, const char *const *names, const int64_t *lengths) {
+  auto *x = new HC();
+  x->h.T.assign(codes, codes + n);
+  int64_t off = 0;
+  for (int i = 0; i < nc; ++i) { x->h.names.push_back(names[i]); x->h.offsets.push_back(off); x->h.lengths.push_back(lengths[i]); off += lengths[i]; }
+  x->h.N = n;
+  std::vector<uint8_t> R(n);
+  for (uint64_t i = 0; i < n; ++i) R[i] = codes[n - 1 - i];
+  if (!cyclicSAHost(x->h.T.data(), n, x->h.sa[0]) || !cyclicSAHost(R.data(), n, x->h.sa[1])) { delete x; return nullptr; }
+  finishIndex(x->h);
+  IndexView &v = x->v;
+  v.occ[0] = x->h.occ[0].data(); v.occ[1] = x->h.occ[1].data();
+  v.sa[0] = x->h.sa[0].data(); v.sa[1] = x->h.sa[1].data();
+  v.text2 = x->h.text2.data(); v.textN = x->h.textN.data();
+  v.contigOff = x->h.offsets.data();
+  v.nContig = (int32_t)x->h.names.size();
+  v.N = n;
+  for (int c = 0; c < 5; ++c) v.C[c] = x->h.C[c];
+  return x;
+}
+
+void *hc_index_fasta(const char *text, uint64_t len) {
+  HostIndex tmp;
+  packFasta(text, len, tmp);
+  std::vector<const char *> nm;
+  for (auto &s : tmp.names) nm.push_back(s.c_str());
+  return hc_index_codes(tmp.T.data(), tmp.N, (int32_t)nm.size(), nm.data(), tmp.lengths.data());
+}
+
+void hc_index_free(void *p) { delete (HC *)p; }
+
+int hc_sa(void *p, int strand, uint32_t *out) {
+  auto *x = (HC *)p;
+  memcpy(out, x->h.sa[strand].data(), x->h.N * 4);
+  return 0;
+}
+
+// Align with the kernel logic on the CPU; output SAM text (malloc'd).  stats[i*4..] = fm, quick, blocks, states
+int hc_align(void *p, float k, int reportType, int numSplit, uint32_t n, const char *const *names, const char *const *seqs,
+             const char *const *quals, char **out, uint64_t *outLen, int32_t *stats) {
+  auto *x = (HC *)p;
+  SearchConfig cfg{};
+  cfg.k = k; cfg.reportType = reportType; cfg.topL = 5; cfg.numSplit = numSplit;
+  cfg.matchScore = 1; cfg.mismatchPenalty = 3; cfg.splitOpenPenalty = 11; cfg.indelEndSkip = 5; cfg.bandWidth = 31;
+  std::vector<int> lens;
+  int kmax = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    int m = 0;
+    for (const char *c = seqs[i]; *c; ++c) m += *c != ' ';
+    lens.push_back(m);
+    int kk = (k > 0 && k < 1) ? (int)floor((double)((float)m * k)) : (int)k;
+    kmax = std::max(kmax, kk);
+  }
+  std::vector<uint64_t> tab;
+  std::vector<uint32_t> base;
+  buildStairTables(lens, kmax, tab, base);
+  StairTables st{tab.data(), base.data(), kmax, 0};
+  Caps caps{65536, 65536, 4096, 4096, 65536, 2 * 4 * 700, 1400};
+  std::vector<uint8_t> scratch(laneBytes<32>(caps));
+  LaneMem<32> L = laneMem<32>(scratch.data(), caps);
+  std::string sam;
+  const int chains = reportType == 0 ? 1 : 4;
+  const int hitCap = chains * (numSplit + 1), cigCap = 64 * chains;
+  std::vector<OutHit> oh(hitCap);
+  std::vector<uint16_t> oc(cigCap);
+  for (uint32_t i = 0; i < n; ++i) {
+    std::vector<uint8_t> codes;
+    for (const char *c = seqs[i]; *c; ++c)
+      if (*c != ' ') codes.push_back(to3bit((unsigned char)*c));
+    OutHeader hd{};
+    BsfLane<32> lane(x->v, cfg, st, L, caps);
+    std::vector<int32_t> rk = x->h.chrRank;
+    lane.chrRank = rk.data();
+    lane.initRead(codes.data(), (int)codes.size());
+    ScanRes sr{};
+    if (lane.quickPhase(&sr, &hd, oh.data(), oc.data())) {
+      lane.searchPhase(sr);
+      lane.writeSearchOutput(&hd, oh.data(), oc.data(), hitCap, cigCap);
+    }
+    if (stats) { stats[i * 4] = hd.fmSearches; stats[i * 4 + 1] = hd.quickSteps; stats[i * 4 + 2] = hd.blocks; stats[i * 4 + 3] = hd.states; }
+    ReadText rt{names[i], strlen(names[i]), seqs[i], strlen(seqs[i]), quals ? quals[i] : nullptr, (quals && quals[i]) ? strlen(quals[i]) : 0};
+    if (!rt.qual) rt.qualLen = 0;
+    if (hd.status == ST_MAPPED) {
+      for (int c = 0; c < hd.nChains; ++c)
+        if (formatChain(x->h, rt, oh.data(), oc.data(), hd.chainHead[c], sam) != 0) return -2;
+    } else if (hd.status == ST_UNMAPPED) {
+      formatUnmapped(rt, sam);
+    } else {
+      fprintf(stderr, "hc: status %d at read %u\n", hd.status, i);
+      return -1 - hd.status;
+    }
+  }
+  *out = (char *)malloc(sam.size() + 1);
+  memcpy(*out, sam.c_str(), sam.size() + 1);
+  *outLen = sam.size();
+  return 0;
+}
+}

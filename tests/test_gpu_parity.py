@@ -1,0 +1,150 @@
+"""GPU parity: the HIP path through the C-ABI against the CPU oracle (bit-exact SAM text), plus
+size-independent properties of the GPU-built index.  Needs an MI355X (`-m gpu`)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+sys.path.insert(0, HERE)
+
+import oracle as O  # noqa: E402
+import synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gwa():
+    import gwa as g
+    return g
+
+
+def _both(codes, names, lengths):
+    import gwa
+    return gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths), O.Index.from_arrays(codes, names, lengths)
+
+
+def _check(gi, oi, reads, **cfg):
+    import gwa
+    c = gwa.AlignmentConfig(**cfg)
+    got = gwa.BidirectionalSuffixFilter(gi, c).align_batch(reads)
+    rt = {"besthit": 0, "allhits": 1, "topl": 2}[c.reportType.lower()]
+    exp = oi.align(reads, O.OrcConfig.default(k=float(c.k), report_type=rt))
+    if got != exp:
+        g, e = got.splitlines(), exp.splitlines()
+        bad = [(a, b) for a, b in zip(g, e) if a != b][:3]
+        raise AssertionError("SAM differs: %d vs %d lines; first diffs: %r" % (len(g), len(e), bad))
+    return got
+
+
+@pytest.fixture(scope="module")
+def random_pair():
+    codes, names, lengths = synth.genome([("c1", 300000), ("c2", 200000)], 1)
+    gi, oi = _both(codes, names, lengths)
+    return codes, names, lengths, gi, oi
+
+
+def test_known_answers_on_gpu(gwa):
+    import json
+    G = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.json")))
+    gi = gwa.FMIndexOnGenome.buildFromSequence("seq", G["bsf"]["reference"])
+    oi = O.Index.from_sequence("seq", G["bsf"]["reference"])
+    reads = [("read", c["query"], None) for c in G["bsf"]["cases"]]
+    _check(gi, oi, reads, k=2.0)
+    # BWAlignTest.align3 (CLI-built index of test2.fa, default k)
+    fa = open(os.path.join(HERE, "golden", "fixtures", "test2.fa")).read()
+    gi2 = gwa.FMIndexOnGenome.buildFromFasta(fa)
+    sam = gwa.BidirectionalSuffixFilter(gi2).align_batch([("read", "TAAAGTAT", None)])
+    f = sam.split("\t")
+    assert (f[1], f[2], f[3]) == ("82", "seq2", "9")
+    assert gi2.samHeader() == "@SQ\tSN:seq1\tLN:27\n@SQ\tSN:seq2\tLN:28\n"
+
+
+def test_gpu_index_sa_matches_oracle(random_pair):
+    codes, names, lengths, gi, oi = random_pair
+    for s in (0, 1):
+        assert np.array_equal(gi.suffixArray(s).astype(np.int64), oi.sa(s))
+
+
+@pytest.mark.parametrize("k", [2.0, 0.1, 0.0])
+def test_random_substitutions(random_pair, k):
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 3000, 100, 2)
+    strs = synth.to_strings(seqs)
+    _check(gi, oi, [(rn[i], strs[i], "I" * 100) for i in range(len(strs))], k=k)
+
+
+def test_indels_150_k5(random_pair):
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 500, 150, config_id=4, indels=True, max_edits=5)
+    strs = synth.to_strings(seqs)
+    _check(gi, oi, [(rn[i], strs[i], "I" * 150) for i in range(len(strs))], k=5.0)
+
+
+@pytest.fixture(scope="module")
+def repetitive_pair():
+    from test_hostcore import repetitive_genome as rg  # noqa
+    rng = np.random.default_rng(11)
+    seg = rng.integers(0, 4, 3000).astype(np.uint8)
+    parts = []
+    for i in range(40):
+        s = seg.copy()
+        mut = rng.integers(0, 3000, rng.integers(0, 60))
+        s[mut] = rng.integers(0, 4, len(mut))
+        parts.append(s)
+        parts.append(rng.integers(0, 4, rng.integers(10, 2000)).astype(np.uint8))
+        if i % 7 == 0:
+            parts.append(np.full(rng.integers(1, 50), 4, np.uint8))
+        if i % 5 == 0:
+            parts.append(np.tile(rng.integers(0, 4, rng.integers(1, 6)).astype(np.uint8), 40))
+    codes = np.concatenate(parts)
+    L = len(codes)
+    names, lengths = ["chrA", "chrB", "chr10"], [L // 3, L // 3, L - 2 * (L // 3)]
+    gi, oi = _both(codes, names, lengths)
+    return codes, gi, oi
+
+
+@pytest.mark.parametrize("m,k,sub", [(100, 2.0, 2), (100, 0.1, 5), (150, 5.0, 5), (50, 0.1, 3)])
+@pytest.mark.parametrize("chim", [False, True])
+def test_repetitive(repetitive_pair, m, k, sub, chim):
+    from test_hostcore import _mk
+    codes, gi, oi = repetitive_pair
+    _check(gi, oi, _mk(codes, 400, m, sub, chim, seed=m * 7 + int(chim)), k=k)
+
+
+@pytest.mark.parametrize("rt", ["allhits", "topl"])
+def test_report_modes(repetitive_pair, rt):
+    from test_hostcore import _mk
+    codes, gi, oi = repetitive_pair
+    _check(gi, oi, _mk(codes, 300, 100, 2, rt == "topl", seed=99), k=2.0, reportType=rt)
+
+
+def test_edge_reads(random_pair):
+    codes, names, lengths, gi, oi = random_pair
+    rng = np.random.default_rng(5)
+    seqs, rn = synth.reads(codes, lengths, 300, 100, 2)
+    strs = synth.to_strings(seqs)
+    reads = []
+    for i in range(300):
+        s = list(strs[i])
+        for j in rng.integers(0, 100, rng.integers(0, 4)):
+            s[j] = "N"
+        reads.append(("n%d" % i, "".join(s), "I" * 100))
+    reads += [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), None) for i in range(100)]
+    reads += [("short", "ACG", None), ("lower", strs[0].lower(), None), ("u", strs[1].replace("T", "U"), None)]
+    # a batch must have quals for all or none
+    _check(gi, oi, [(a, b, c if c else "I" * len(b)) for a, b, c in reads], k=2.0)
+
+
+def test_ecoli_c1_exact(gwa):
+    """Config 1: E. coli-size index, 10k exact 100 bp reads (-k 0)."""
+    codes, names, lengths = synth.genome(synth.ECOLI, 1)
+    gi, oi = _both(codes, names, lengths)
+    seqs, rn = synth.reads(codes, lengths, 10000, 100, 0, config_id=1)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
+    sam = _check(gi, oi, reads, k=0.0)
+    assert all(l.split("\t")[1] in ("66", "82") for l in sam.splitlines())

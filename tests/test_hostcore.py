@@ -1,0 +1,113 @@
+"""The kernel logic (bsf_core.h) compiled for the CPU, against the oracle: random and
+repetitive references, substitutions/indels/N/chimeric reads, all report modes.  This is a
+debugging harness for the device code (the GPU parity tests are tests/test_gpu_parity.py)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "hostcore"))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+
+import oracle as O  # noqa: E402
+import synth  # noqa: E402
+import hostcore  # noqa: E402
+
+
+def _cmp(codes, names, lengths, reads, k, rt=0):
+    oi = O.Index.from_arrays(codes, names, lengths)
+    hc = hostcore.HostCore(codes, names, lengths)
+    b = oi.align(reads, O.OrcConfig.default(k=k, report_type=rt))
+    a = hc.align(reads, k=k, report_type=rt)
+    assert a == b
+
+
+@pytest.fixture(scope="module")
+def random_genome():
+    return synth.genome([("c1", 300000), ("c2", 200000)], 1)
+
+
+@pytest.fixture(scope="module")
+def repetitive_genome():
+    rng = np.random.default_rng(11)
+    seg = rng.integers(0, 4, 3000).astype(np.uint8)
+    parts = []
+    for i in range(40):
+        s = seg.copy()
+        mut = rng.integers(0, 3000, rng.integers(0, 60))
+        s[mut] = rng.integers(0, 4, len(mut))
+        parts.append(s)
+        parts.append(rng.integers(0, 4, rng.integers(10, 2000)).astype(np.uint8))
+        if i % 7 == 0:
+            parts.append(np.full(rng.integers(1, 50), 4, np.uint8))
+        if i % 5 == 0:
+            parts.append(np.tile(rng.integers(0, 4, rng.integers(1, 6)).astype(np.uint8), 40))
+    codes = np.concatenate(parts)
+    L = len(codes)
+    return codes, ["chrA", "chrB", "chr10"], [L // 3, L // 3, L - 2 * (L // 3)]
+
+
+def _mk(codes, n, m, sub, chim, seed):
+    rng = np.random.default_rng(seed)
+    L = len(codes)
+    out = []
+    for i in range(n):
+        if chim:
+            a, b, cut = rng.integers(0, L - m), rng.integers(0, L - m), rng.integers(8, m - 8)
+            s = np.concatenate([codes[a:a + cut], codes[b + cut:b + m]])
+        else:
+            a = rng.integers(0, L - m)
+            s = codes[a:a + m].copy()
+        for j in rng.integers(0, m, rng.integers(0, sub + 1)):
+            if s[j] < 4:
+                s[j] = (s[j] + rng.integers(1, 4)) % 4
+        if rng.random() < 0.5:
+            s = synth.COMP[s[::-1]]
+        out.append(("q%05d" % i, synth.SYM[s].tobytes().decode(), "I" * m))
+    return out
+
+
+@pytest.mark.parametrize("k", [2.0, 0.1, 0.0])
+def test_random_genome_substitutions(random_genome, k):
+    codes, names, lengths = random_genome
+    seqs, rn = synth.reads(codes, lengths, 600, 100, 2)
+    strs = synth.to_strings(seqs)
+    _cmp(codes, names, lengths, [(rn[i], strs[i], "I" * 100) for i in range(len(strs))], k)
+
+
+def test_random_genome_indels_150(random_genome):
+    codes, names, lengths = random_genome
+    seqs, rn = synth.reads(codes, lengths, 200, 150, config_id=4, indels=True, max_edits=5)
+    strs = synth.to_strings(seqs)
+    _cmp(codes, names, lengths, [(rn[i], strs[i], None) for i in range(len(strs))], 5.0)
+
+
+@pytest.mark.parametrize("m,k,sub", [(100, 2.0, 2), (100, 0.1, 5), (150, 5.0, 5), (50, 0.1, 3), (36, 2.0, 2)])
+@pytest.mark.parametrize("chim", [False, True])
+def test_repetitive_genome(repetitive_genome, m, k, sub, chim):
+    codes, names, lengths = repetitive_genome
+    _cmp(codes, names, lengths, _mk(codes, 200, m, sub, chim, seed=m * 7 + int(chim)), k)
+
+
+@pytest.mark.parametrize("rt", [1, 2])
+def test_report_modes(repetitive_genome, rt):
+    codes, names, lengths = repetitive_genome
+    _cmp(codes, names, lengths, _mk(codes, 200, 100, 2, rt == 2, seed=99), 2.0, rt=rt)
+
+
+def test_reads_with_n_and_unmappable(random_genome):
+    codes, names, lengths = random_genome
+    rng = np.random.default_rng(5)
+    seqs, rn = synth.reads(codes, lengths, 200, 100, 2)
+    strs = synth.to_strings(seqs)
+    reads = []
+    for i in range(200):
+        s = list(strs[i])
+        for j in rng.integers(0, 100, rng.integers(0, 4)):
+            s[j] = "N"
+        reads.append(("n%d" % i, "".join(s), "I" * 100))
+    reads += [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), None) for i in range(100)]
+    reads += [("e0", "", None), ("short", "ACG", None), ("lower", strs[0].lower(), None)]
+    _cmp(codes, names, lengths, reads, 2.0)
