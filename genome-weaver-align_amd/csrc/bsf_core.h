@@ -178,6 +178,16 @@ struct BsfLane {
   int status;  // ST_*
   // instrumentation
   int quickSteps, blocks, saReads;
+  // debug trace (nullptr in production launches): 4 words per event
+  uint32_t *trace = nullptr;
+  int traceCap = 0, traceN = 0;
+  GWA_HD void tr(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if (!trace || traceN + 4 > traceCap) return;
+    trace[traceN++] = a; trace[traceN++] = b; trace[traceN++] = c; trace[traceN++] = d;
+  }
+  GWA_HD uint32_t curWord(const DState<R> &d) const {
+    return (uint32_t)d.flag | ((uint32_t)d.start << 8) | ((uint32_t)d.end << 16) | ((uint32_t)d.cursor << 24);
+  }
 
   GWA_HD BsfLane(const IndexView &ix_, const SearchConfig &c_, const StairTables &s_, LaneMem<R> L_, Caps caps_)
       : ix(ix_), cfg(c_), st(s_), L(L_), caps(caps_) {}
@@ -449,7 +459,9 @@ struct BsfLane {
     const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
     uint64_t lb = 0, ub = ix.N;
     int mark = 0, nmm = 0;
-    bool have = false;
+    // longestMatch bookkeeping kept branch-free (loop-carried i1 flags in this divergent loop were
+    // mis-lowered by the gfx950 backend in our tests); `have` is an int 0/1.
+    int have = 0;
     int lmS = 0, lmE = 0;
     int i = 0;
     for (; i < m; ++i) {
@@ -466,15 +478,22 @@ struct BsfLane {
       }
       uint64_t nub = ix.C[ch] + rankOne(B, ub, ch);
       ++quickSteps;
-      lb = nlb; ub = nub;
-      if (lb >= ub) {
-        nmm++;
-        if (!have || (lmE - lmS) < (i - mark)) { have = true; lmS = mark; lmE = i; }
-        lb = 0; ub = ix.N;
-        mark = i + 1;
-      }
+      tr(16 + strand, (uint32_t)(i | (ch << 16)), (uint32_t)nlb, (uint32_t)nub);
+      const int empty = nlb >= nub ? 1 : 0;
+      const int better = empty & ((have ^ 1) | ((lmE - lmS) < (i - mark) ? 1 : 0));
+      lmS = better ? mark : lmS;
+      lmE = better ? i : lmE;
+      have |= empty;
+      nmm += empty;
+      lb = empty ? 0 : nlb;
+      ub = empty ? ix.N : nub;
+      mark = empty ? i + 1 : mark;
     }
-    if (!have || (lmE - lmS) < (i - mark)) { lmS = mark; lmE = i; }
+    {
+      const int better = (have ^ 1) | ((lmE - lmS) < (i - mark) ? 1 : 0);
+      lmS = better ? mark : lmS;
+      lmE = better ? i : lmE;
+    }
     Scan s;
     s.lb = lb; s.ub = ub; s.numMismatches = nmm; s.lmStart = lmS;
     return s;
@@ -613,7 +632,7 @@ struct BsfLane {
     for (int i = 0; i < bMax; ++i) { int v = mq - ((i + 1) * w) + kb; scoreBoundary[i] = v > 0 ? v : 0; }
     int bCeil = (kb + w - 1) / w;
     if (bCeil < 1) bCeil = 1;
-    bool have = false;
+    int have = 0;  // int, not bool: see quickScan
     int bestTail = 0, bestDiff = 0;
     auto alignBlock = [&](int j, int ch, int r, int hin) -> int {
       uint64_t vpv = VP(r, j), vnv = VN(r, j);
@@ -649,7 +668,7 @@ struct BsfLane {
         while (bCeil > 1 && D[bCeil - 1] > scoreBoundary[bCeil - 1] + w) --bCeil;
       }
       if (bCeil == bMax) {
-        if (!have) { have = true; bestTail = j; bestDiff = D[bCeil - 1]; continue; }
+        if (!have) { have = 1; bestTail = j; bestDiff = D[bCeil - 1]; continue; }
         if (bestDiff > D[bCeil - 1]) { bestTail = j; bestDiff = D[bCeil - 1]; }
       }
     }
@@ -802,10 +821,10 @@ struct BsfLane {
     }
     const int mPos = kk + frag - progress;
     int rem = -1;
-    bool hm = false;
+    int hm = 0;
     if (mPos < 64) {
       for (int nm = 0; nm < height; ++nm)
-        if ((next[nm] & jshl(1, mPos)) != 0) { rem = nm; hm = true; break; }
+        if (rem < 0 && (next[nm] & jshl(1, mPos)) != 0) { rem = nm; hm = 1; }
     }
     if (!hm) {
       int mk = minKwithMatch < minKwithProgress ? minKwithMatch : minKwithProgress;
@@ -822,7 +841,7 @@ struct BsfLane {
       *outH = nh;
     }
     *outKOff = kOff + rem;
-    *hasMatch = hm;
+    *hasMatch = hm != 0;
     return true;
   }
 
@@ -876,7 +895,9 @@ struct BsfLane {
     d.meta = 0;
     nextSi(cs, ch, d);
     ++numFMIndexSearches;
-    if (!nfaNext(cs, ch, strand, rows, &nh, &nko, &hm)) return -1;
+    tr(2, (uint32_t)ch, d.lb[0] ^ (d.ub[1] * 3u) ^ (d.lb[2] * 7u) ^ (d.ub[3] * 11u) ^ d.bBase, (uint32_t)(d.meta & 3));
+    if (!nfaNext(cs, ch, strand, rows, &nh, &nko, &hm)) { tr(3, 0, 0, 0); return -1; }
+    tr(4, (uint32_t)nh | ((uint32_t)nko << 8) | ((uint32_t)hm << 16), (uint32_t)rows[0], (uint32_t)(nh > 1 ? rows[1] : 0));
     int id = allocState();
     if (id < 0) return -2;
     // Cursor.next (S/Cursor.java:158-180)
@@ -1051,13 +1072,14 @@ struct BsfLane {
       if (numFMIndexSearches > upper) break;
       const int base = queuePoll();
       int c = base;
+      tr(1, (uint32_t)base, curWord(S(base)), (uint32_t)S(base).state);
       {
         int nx = c;
-        bool reported = false;
+        int reported = 0;
         while (hasHit(nx) || isClipped(nx) || cRemaining(S(nx)) == 0) {
           if (S(nx).nextSplit < 0) {
             if (!reportAlignment(c)) return;
-            reported = true;
+            reported = 1;
             break;
           }
           nx = S(nx).nextSplit;
@@ -1075,7 +1097,7 @@ struct BsfLane {
       }
       const int strand = cStrand(S(c));
       const int nextBase = q(strand, cNextIdx(S(c)));
-      bool advanced = false;
+      int advanced = 0;
       {
         int ch = nextBase;
         if (!isChecked(c, ch)) {
@@ -1083,7 +1105,7 @@ struct BsfLane {
           if (!siIsEmpty(S(c), ch)) {
             int ns = nextState(c, ch);
             if (ns == -2) return;
-            if (ns >= 0) { queueAdd(update(base, c, ns)); advanced = true; }
+            if (ns >= 0) { queueAdd(update(base, c, ns)); advanced = 1; }
           }
         }
       }

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -361,8 +362,18 @@ int gwa_batch_run(gwa_batch_t *b) {
     HIPCHK(hipEventCreate(&e2));
     HIPCHK(hipMemsetAsync(b->d_count, 0, 8 * sizeof(uint32_t), s));
     HIPCHK(hipEventRecord(e0, s));
+    const char *qtre = getenv("GWA_QTRACE_READ");
+    static uint32_t *d_qtrace = nullptr;
+    if (qtre && !d_qtrace) { HIPCHK(hipMalloc(&d_qtrace, 4 * 65540)); HIPCHK(hipMemset(d_qtrace, 0, 4 * 65540)); }
     launchQuickscan(ix->view, b->scfg, rv, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, b->d_list[0],
-                    b->d_count, s);
+                    b->d_count, s, qtre ? d_qtrace : nullptr, qtre ? atoi(qtre) : -1);
+    if (qtre) {
+      std::vector<uint32_t> tv(65537);
+      HIPCHK(hipMemcpyAsync(tv.data(), d_qtrace, 4 * 65537, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      FILE *tf = fopen("gpurun_out/gpu_qtrace.bin", "wb");
+      if (tf) { fwrite(tv.data(), 4, 1 + tv[0], tf); fclose(tf); }
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
     uint32_t nSearch = 0;
@@ -396,8 +407,20 @@ int gwa_batch_run(gwa_batch_t *b) {
       }
       uint32_t *ovfCount = b->d_count + 1 + t;
       HIPCHK(hipEventRecord(e1, s));
+      static uint32_t *d_trace = nullptr;
+      const char *tre = getenv("GWA_TRACE_READ");
+      int traceRead = tre ? atoi(tre) : -1;
+      if (traceRead >= 0 && !d_trace) { HIPCHK(hipMalloc(&d_trace, 4 * 65540)); HIPCHK(hipMemset(d_trace, 0, 4 * 65540)); }
       launchSearch(b->R, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
-                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_list[cur ^ 1], ovfCount, s);
+                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_list[cur ^ 1], ovfCount, s,
+                   traceRead >= 0 ? d_trace : nullptr, traceRead);
+      if (traceRead >= 0) {
+        std::vector<uint32_t> tv(65537);
+        HIPCHK(hipMemcpyAsync(tv.data(), d_trace, 4 * 65537, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        FILE *tf = fopen(getenv("GWA_TRACE_FILE") ? getenv("GWA_TRACE_FILE") : "gwa_trace.bin", "wb");
+        if (tf) { fwrite(tv.data(), 4, 1 + tv[0], tf); fclose(tf); }
+      }
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(e2, s));
       uint32_t nOvf = 0;
@@ -522,6 +545,25 @@ int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) {
     }
     out->line_off[n] = pos;
     out->sam[total] = 0;
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
+
+int gwa_batch_read_counters(gwa_batch_t *b, int32_t *out) {
+  try {
+    if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
+    fetch(b);
+    std::vector<ScanRes> sr(b->n);
+    HIPCHK(hipMemcpy(sr.data(), b->d_sres, b->n * sizeof(ScanRes), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < b->n; ++i) {
+      const OutHeader &h = b->oh[i];
+      int32_t *o = out + (size_t)i * 12;
+      o[8] = sr[i].nmF; o[9] = sr[i].lmF; o[10] = sr[i].nmR; o[11] = sr[i].lmR;
+      o[0] = h.status; o[1] = h.fmSearches; o[2] = h.quickSteps; o[3] = h.blocks; o[4] = h.searchBlocks;
+      o[5] = h.states; o[6] = h.saReads; o[7] = h.nHits;
+    }
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());

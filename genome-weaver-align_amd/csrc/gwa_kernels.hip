@@ -32,7 +32,8 @@ __device__ __forceinline__ void waveAppend(bool need, uint32_t value, uint32_t *
 
 __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
                                                            OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
-                                                           uint32_t *searchList, uint32_t *searchCount) {
+                                                           uint32_t *searchList, uint32_t *searchCount, uint32_t *trace,
+                                                           int traceRead) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   bool need = false;
   if (r < reads.n) {
@@ -47,8 +48,10 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
       LaneMem<4> L{};
       Caps caps{};
       BsfLane<4> lane(ix, cfg, st, L, caps);
+      if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
       lane.initRead(reads.codes + o, m);
       need = lane.quickPhase(sres + r, h, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap) != 0;
+      if (lane.trace) trace[0] = (uint32_t)lane.traceN;
     }
   }
   waveAppend(need, r, searchList, searchCount);
@@ -59,7 +62,7 @@ __global__ void __launch_bounds__(256) bsf_search_kernel(IndexView ix, SearchCon
                                                          const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                                                          uint64_t laneStride, Caps caps, OutHeader *oh, OutHit *ohits,
                                                          uint16_t *ocig, int hitCap, int cigCap, const int32_t *chrRank,
-                                                         uint32_t *ovfList, uint32_t *ovfCount) {
+                                                         uint32_t *ovfList, uint32_t *ovfCount, uint32_t *trace, int traceRead) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
   LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, caps);
@@ -75,9 +78,11 @@ __global__ void __launch_bounds__(256) bsf_search_kernel(IndexView ix, SearchCon
       const int m = (int)(reads.off[r + 1] - o);
       BsfLane<R> lane(ix, cfg, st, L, caps);
       lane.chrRank = chrRank;
+      if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
       lane.initRead(reads.codes + o, m);
       lane.searchPhase(sres[r]);
       lane.writeSearchOutput(oh + r, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap, hitCap, cigCap);
+      if (lane.trace) trace[0] = (uint32_t)lane.traceN;
       ovf = oh[r].status == ST_OVERFLOW;
     }
     waveAppend(ovf, r, ovfList, ovfCount);
@@ -86,24 +91,25 @@ __global__ void __launch_bounds__(256) bsf_search_kernel(IndexView ix, SearchCon
 
 void launchQuickscan(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
                      OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap, uint32_t *searchList, uint32_t *searchCount,
-                     hipStream_t s) {
+                     hipStream_t s, uint32_t *trace, int traceRead) {
   if (reads.n == 0) return;
   dim3 grid((reads.n + 255) / 256);
   hipLaunchKernelGGL(fm_quickscan_kernel, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, ohits, ocig, hitCap, cigCap,
-                     searchList, searchCount);
+                     searchList, searchCount, trace, traceRead);
 }
 
 void launchSearch(int R, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                   uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
-                  const int32_t *chrRank, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s) {
+                  const int32_t *chrRank, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s, uint32_t *trace,
+                  int traceRead) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
   switch (R) {
 #define GWA_CASE(RR)                                                                                                  \
   case RR:                                                                                                            \
     hipLaunchKernelGGL(bsf_search_kernel<RR>, grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n, scratch,     \
-                       laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, ovfList, ovfCount);                \
+                       laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, ovfList, ovfCount, trace, traceRead);                \
     break;
     GWA_CASE(4)
     GWA_CASE(8)

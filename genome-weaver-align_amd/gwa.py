@@ -49,7 +49,8 @@ _lib = None
 EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_index_build_fasta", "gwa_index_open",
            "gwa_index_build_codes", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
            "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
-           "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free"]
+           "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
+           "gwa_batch_read_counters"]
 
 
 def lib():
@@ -79,6 +80,7 @@ def lib():
         L.gwa_batch_stats.argtypes = [V, P(BatchStats)]
         L.gwa_batch_results.argtypes = [V, P(_Results)]
         L.gwa_batch_free.argtypes = [V]
+        L.gwa_batch_read_counters.argtypes = [V, V]
         _lib = L
     return _lib
 
@@ -267,6 +269,7 @@ class Batch:
     def __init__(self, fmIndex, config, reads):
         self._keep = []
         r = _reads_struct(reads, self._keep)
+        self.n = len(reads)
         self.h = ctypes.c_void_p()
         c = config._c()
         _check(lib().gwa_batch_create(fmIndex.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(self.h)))
@@ -283,6 +286,14 @@ class Batch:
         res = _Results()
         _check(lib().gwa_batch_results(self.h, ctypes.byref(res)))
         return _take_results(res)
+
+    def read_counters(self):
+        """per read: status, fm_searches, quick_steps, quickscan_blocks, search_blocks, states, sa_reads, n_hits"""
+        import numpy as np
+        n = ctypes.c_uint32()
+        out = np.zeros((self.n, 12), dtype=np.int32)
+        _check(lib().gwa_batch_read_counters(self.h, out.ctypes.data))
+        return out
 
     def close(self):
         if self.h:

@@ -101,6 +101,10 @@ int gwa_batch_run(gwa_batch_t *b);
 int gwa_batch_stats(const gwa_batch_t *b, gwa_batch_stats_t *st);
 int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out);
 void gwa_batch_free(gwa_batch_t *b);
+/* Instrumentation: per-read counters after gwa_batch_run, 12 int32 per read:
+ * status, fm_searches, quick_steps, quickscan_blocks, search_blocks, states, sa_reads, n_hits,
+ * quick-scan mismatches/longest-match start (forward, reverse) -- the latter only for searched reads. */
+int gwa_batch_read_counters(gwa_batch_t *b, int32_t *out);
 
 #ifdef __cplusplus
 }

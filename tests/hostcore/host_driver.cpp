@@ -19,6 +19,64 @@ struct HC {
   IndexView v{};
 };
 
+// the GPU's capacity tiers (gwa_api.cpp kTiers) replayed on the CPU
+template <int R>
+static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int maxM, int kmax, uint32_t n,
+                  const char *const *names, const char *const *seqs, const char *const *quals, std::string &sam,
+                  int32_t *stats) {
+  const int bMax = std::max(1, (maxM + 63) / 64), nref = maxM + 2 * kmax + 2;
+  const int dpw = 2 * bMax * (nref + 1), path = ((maxM + nref + 8) + 7) & ~7;
+  const Caps tiers[3] = {{256, 256, 32, 32, 512, dpw, path}, {4096, 4096, 256, 256, 4096, dpw, path},
+                         {65536, 65536, 4096, 4096, 65536, dpw, path}};
+  std::vector<uint8_t> scratch(laneBytes<R>(tiers[2]) + 4096);
+  const int chains = cfg.reportType == 0 ? 1 : 4;
+  const int hitCap = chains * (cfg.numSplit + 1), cigCap = 64 * chains;
+  std::vector<OutHit> oh(hitCap);
+  std::vector<uint16_t> oc(cigCap);
+  std::vector<int32_t> rk = x->h.chrRank;
+  for (uint32_t i = 0; i < n; ++i) {
+    std::vector<uint8_t> codes;
+    for (const char *c = seqs[i]; *c; ++c)
+      if (*c != ' ') codes.push_back(to3bit((unsigned char)*c));
+    OutHeader hd{};
+    std::vector<uint32_t> tv(65537, 0);
+    bool traced = false;
+    for (int t = 0; t < 3; ++t) {
+      LaneMem<R> L = laneMem<R>(scratch.data(), tiers[t]);
+      BsfLane<R> lane(x->v, cfg, st, L, tiers[t]);
+      lane.chrRank = rk.data();
+      const char *tre = getenv("GWA_TRACE_READ");
+      const char *qtre = getenv("GWA_QTRACE_READ");
+      if ((tre && atoi(tre) == (int)i) || (qtre && atoi(qtre) == (int)i)) { lane.trace = tv.data() + 1; lane.traceCap = 65536; traced = true; }
+      lane.initRead(codes.data(), (int)codes.size());
+      ScanRes sr{};
+      if (lane.quickPhase(&sr, &hd, oh.data(), oc.data())) {
+        lane.searchPhase(sr);
+        lane.writeSearchOutput(&hd, oh.data(), oc.data(), hitCap, cigCap);
+      }
+      if (traced) tv[0] = (uint32_t)lane.traceN;
+      if (hd.status != ST_OVERFLOW) break;
+    }
+    if (traced) {
+      FILE *tf = fopen("hc_trace.bin", "wb");
+      if (tf) { fwrite(tv.data(), 4, 1 + tv[0], tf); fclose(tf); }
+    }
+    if (stats) { stats[i * 4] = hd.fmSearches; stats[i * 4 + 1] = hd.quickSteps; stats[i * 4 + 2] = hd.searchBlocks; stats[i * 4 + 3] = hd.states; }
+    ReadText rt{names[i], strlen(names[i]), seqs[i], strlen(seqs[i]), quals ? quals[i] : nullptr, (quals && quals[i]) ? strlen(quals[i]) : 0};
+    if (!rt.qual) rt.qualLen = 0;
+    if (hd.status == ST_MAPPED) {
+      for (int c = 0; c < hd.nChains; ++c)
+        if (formatChain(x->h, rt, oh.data(), oc.data(), hd.chainHead[c], sam) != 0) return -2;
+    } else if (hd.status == ST_UNMAPPED) {
+      formatUnmapped(rt, sam);
+    } else {
+      fprintf(stderr, "hc: status %d at read %u\n", hd.status, i);
+      return -1 - hd.status;
+    }
+  }
+  return 0;
+}
+
 extern "C" {
 
 void *hc_index_codes(const uint8_t *codes, uint64_t n, int32_t nc, const char *const *names, const int64_t *lengths) {
@@ -78,41 +136,18 @@ int hc_align(void *p, float k, int reportType, int numSplit, uint32_t n, const c
   std::vector<uint32_t> base;
   buildStairTables(lens, kmax, tab, base);
   StairTables st{tab.data(), base.data(), kmax, 0};
-  Caps caps{65536, 65536, 4096, 4096, 65536, 2 * 4 * 700, 1400};
-  std::vector<uint8_t> scratch(laneBytes<32>(caps));
-  LaneMem<32> L = laneMem<32>(scratch.data(), caps);
   std::string sam;
-  const int chains = reportType == 0 ? 1 : 4;
-  const int hitCap = chains * (numSplit + 1), cigCap = 64 * chains;
-  std::vector<OutHit> oh(hitCap);
-  std::vector<uint16_t> oc(cigCap);
-  for (uint32_t i = 0; i < n; ++i) {
-    std::vector<uint8_t> codes;
-    for (const char *c = seqs[i]; *c; ++c)
-      if (*c != ' ') codes.push_back(to3bit((unsigned char)*c));
-    OutHeader hd{};
-    BsfLane<32> lane(x->v, cfg, st, L, caps);
-    std::vector<int32_t> rk = x->h.chrRank;
-    lane.chrRank = rk.data();
-    lane.initRead(codes.data(), (int)codes.size());
-    ScanRes sr{};
-    if (lane.quickPhase(&sr, &hd, oh.data(), oc.data())) {
-      lane.searchPhase(sr);
-      lane.writeSearchOutput(&hd, oh.data(), oc.data(), hitCap, cigCap);
-    }
-    if (stats) { stats[i * 4] = hd.fmSearches; stats[i * 4 + 1] = hd.quickSteps; stats[i * 4 + 2] = hd.blocks; stats[i * 4 + 3] = hd.states; }
-    ReadText rt{names[i], strlen(names[i]), seqs[i], strlen(seqs[i]), quals ? quals[i] : nullptr, (quals && quals[i]) ? strlen(quals[i]) : 0};
-    if (!rt.qual) rt.qualLen = 0;
-    if (hd.status == ST_MAPPED) {
-      for (int c = 0; c < hd.nChains; ++c)
-        if (formatChain(x->h, rt, oh.data(), oc.data(), hd.chainHead[c], sam) != 0) return -2;
-    } else if (hd.status == ST_UNMAPPED) {
-      formatUnmapped(rt, sam);
-    } else {
-      fprintf(stderr, "hc: status %d at read %u\n", hd.status, i);
-      return -1 - hd.status;
-    }
+  int maxM = 1;
+  for (int m : lens) maxM = std::max(maxM, m);
+  int R = kmax + 1 <= 4 ? 4 : kmax + 1 <= 8 ? 8 : kmax + 1 <= 16 ? 16 : 32;
+  int rc = 0;
+  switch (R) {
+    case 4: rc = runAll<4>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 8: rc = runAll<8>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 16: rc = runAll<16>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    default: rc = runAll<32>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
   }
+  if (rc != 0) return rc;
   *out = (char *)malloc(sam.size() + 1);
   memcpy(*out, sam.c_str(), sam.size() + 1);
   *outLen = sam.size();
