@@ -71,14 +71,19 @@ def main():
 
     cfg = gwa.AlignmentConfig(k=args.k)
     # synthetic 100 bp reads, 0-2 substitutions, shard = rank
+    m = 100
     t0 = time.time()
-    seqs, rn = synth.reads(codes, lengths, reads_per_step, 100, 2, config_id=2, shard=rank)
-    strs = synth.to_strings(seqs)
-    reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
+    seqs = synth.reads_codes(codes, lengths, reads_per_step, m, 2, config_id=2, shard=rank)
+    seq_blob = synth.SYM[seqs].tobytes()
+    seq_off = np.arange(0, m * (reads_per_step + 1), m, dtype=np.uint64)
+    name_blob, name_off = synth.name_blob(reads_per_step)
+    qual_blob = b"I" * (m * reads_per_step)
     log("reads generated in %.1fs" % (time.time() - t0))
     t0 = time.time()
-    batch = gwa.Batch(gi, cfg, reads)
+    batch = gwa.Batch(gi, cfg, blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
     log("batch resident in HBM: %.1fs" % (time.time() - t0))
+    nchk = min(max(args.check, args.cpu_sample if not args.no_cpu else 0), reads_per_step)
+    reads = [(name_blob[10 * i:10 * i + 10].decode(), seq_blob[m * i:m * i + m].decode(), "I" * m) for i in range(nchk)]
 
     for _ in range(args.warmup):
         batch.run()
@@ -105,7 +110,8 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         dt = float(t[0])
 
-    sam, off = batch.results()
+    nres = min(args.check, reads_per_step)
+    sam, off = batch.results(0, nres)
     st = batch.stats()
     total_reads = reads_per_step * args.steps * world
     value = total_reads / dt
@@ -118,9 +124,9 @@ def main():
         t0 = time.time()
         oi = O.Index.from_arrays(codes, names, lengths, sa_f=gi.suffixArray(0), sa_r=gi.suffixArray(1))
         t_oidx = time.time() - t0
-        nchk = min(args.check, len(reads))
+        nchk = nres
         exp = oi.align(reads[:nchk], O.OrcConfig.default(k=args.k))
-        got = sam[:int(off[nchk])]
+        got = sam
         parity = {"reads": nchk, "identical": got == exp}
         log("parity on %d reads: %s (oracle index %.1fs)" % (nchk, got == exp, t_oidx))
 

@@ -120,26 +120,54 @@ static void freeIndexDev(gwa_index *ix) {
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
 }
 
-// Build SAs (GPU for large texts), Occ blocks, text; upload everything to HBM.
+namespace gwa {
+bool cyclicSAGpu(const uint8_t *d_T, uint64_t N, uint32_t *d_sa, int alphabetBits, hipStream_t s);
+void reverseTextGpu(const uint8_t *d_T, uint64_t N, uint8_t *d_R, hipStream_t s);
+void buildOccGpu(const uint8_t *d_T, const uint32_t *d_sa, uint64_t N, OccBlock *d_occ, hipStream_t s);
+void packTextGpu(const uint8_t *d_T, uint64_t N, uint64_t *d_text2, uint64_t *d_textN, hipStream_t s);
+}  // namespace gwa
+
+// Index construction in HBM (the `bwt` command's work, A/BWTransform.java:72-179): upload the
+// packed text once, build the reversed text, both cyclic SAs, both Occ-block arrays and the
+// 2-bit text on the GPU.
 static void finishAndUpload(gwa_index *ix) {
   HostIndex &h = ix->host;
   if (h.N == 0) throw std::runtime_error("empty reference");
   if (h.N >= 0xFFFFFFFFull) throw std::runtime_error("reference longer than 2^32-2 bases is not supported");
   HIPCHK(hipSetDevice(ix->device));
   HIPCHK(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
-  std::vector<uint8_t> R(h.N);
-  for (uint64_t i = 0; i < h.N; ++i) R[i] = h.T[h.N - 1 - i];
-  // cyclic suffix arrays (A/sais/CyclicSAIS.java:223-431 computes the same unique order)
-  if (!cyclicSAHost(h.T.data(), h.N, h.sa[0]) || !cyclicSAHost(R.data(), h.N, h.sa[1]))
-    throw std::runtime_error("reference text is periodic (cyclic rotations tie): unsupported");
-  finishIndex(h);
   hipStream_t s = ix->stream;
-  for (int k = 0; k < 2; ++k) {
-    ix->d_occ[k] = devUpload(h.occ[k], s, &ix->bytes);
-    ix->d_sa[k] = devUpload(h.sa[k], s, &ix->bytes);
+  const uint64_t N = h.N;
+  uint8_t *dT = devAlloc<uint8_t>(N);
+  uint8_t *dR = devAlloc<uint8_t>(N);
+  HIPCHK(hipMemcpyAsync(dT, h.T.data(), N, hipMemcpyHostToDevice, s));
+  reverseTextGpu(dT, N, dR, s);
+  ix->d_sa[0] = devAlloc<uint32_t>(N, &ix->bytes);
+  ix->d_sa[1] = devAlloc<uint32_t>(N, &ix->bytes);
+  // cyclic suffix arrays (A/sais/CyclicSAIS.java:223-431 computes the same unique order)
+  if (!cyclicSAGpu(dT, N, ix->d_sa[0], 3, s) || !cyclicSAGpu(dR, N, ix->d_sa[1], 3, s)) {
+    (void)hipFree(dT);
+    (void)hipFree(dR);
+    throw std::runtime_error("reference text is periodic (cyclic rotations tie): unsupported");
   }
-  ix->d_text2 = devUpload(h.text2, s, &ix->bytes);
-  ix->d_textN = devUpload(h.textN, s, &ix->bytes);
+  const uint64_t nb = N / 128 + 1;
+  ix->d_occ[0] = devAlloc<OccBlock>(nb, &ix->bytes);
+  ix->d_occ[1] = devAlloc<OccBlock>(nb, &ix->bytes);
+  buildOccGpu(dT, ix->d_sa[0], N, ix->d_occ[0], s);
+  buildOccGpu(dR, ix->d_sa[1], N, ix->d_occ[1], s);
+  const uint64_t nw = N / 64 + 1;
+  ix->d_text2 = devAlloc<uint64_t>(2 * nw, &ix->bytes);
+  ix->d_textN = devAlloc<uint64_t>(nw, &ix->bytes);
+  packTextGpu(dT, N, ix->d_text2, ix->d_textN, s);
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(dT);
+  (void)hipFree(dR);
+  // CharacterCount.C (A/CharacterCount.java:41-50)
+  uint64_t count[5] = {0, 0, 0, 0, 0};
+  for (uint64_t i = 0; i < N; ++i) count[h.T[i] > 4 ? 4 : h.T[i]]++;
+  uint64_t sum = 0;
+  for (int c = 0; c < 5; ++c) { h.C[c] = sum; sum += count[c]; }
+  rankNames(h);
   ix->d_contig = devUpload(h.offsets, s, &ix->bytes);
   ix->d_chrRank = devUpload(h.chrRank, s, &ix->bytes);
   HIPCHK(hipStreamSynchronize(s));
@@ -149,12 +177,9 @@ static void finishAndUpload(gwa_index *ix) {
   v.text2 = ix->d_text2; v.textN = ix->d_textN;
   v.contigOff = ix->d_contig;
   v.nContig = (int32_t)h.names.size();
-  v.N = h.N;
+  v.N = N;
   for (int c = 0; c < 5; ++c) v.C[c] = h.C[c];
-  // host copies no longer needed except T (SA export) and the contig table
-  for (int k = 0; k < 2; ++k) { std::vector<OccBlock>().swap(h.occ[k]); }
-  std::vector<uint64_t>().swap(h.text2);
-  std::vector<uint64_t>().swap(h.textN);
+  std::vector<uint8_t>().swap(h.T);  // the text lives in HBM from here on
 }
 
 extern "C" {
@@ -478,12 +503,15 @@ static int fetch(gwa_batch *b) {
   return 0;
 }
 
-int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) {
+int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) { return gwa_batch_results_range(b, 0, b->n, out); }
+
+int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out) {
   try {
     if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
+    if ((uint64_t)first + count > b->n) throw std::runtime_error("result range out of bounds");
     fetch(b);
-    const uint32_t n = b->n;
-    for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t n = count;
+    for (uint32_t i = first; i < first + n; ++i) {
       int stt = b->oh[i].status;
       if (stt == ST_ERROR || stt == ST_OVERFLOW || stt == ST_TOO_LONG) {
         std::string nm(b->names.data() + (b->nameOff[i] - b->nameOff[0]), b->nameOff[i + 1] - b->nameOff[i]);
@@ -498,7 +526,7 @@ int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) {
     std::vector<std::vector<uint64_t>> lens(nt);
     std::atomic<int> bad{-1};
     auto work = [&](unsigned t) {
-      uint32_t a = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
+      uint32_t a = first + (uint32_t)((uint64_t)n * t / nt), e = first + (uint32_t)((uint64_t)n * (t + 1) / nt);
       std::string &o = parts[t];
       o.reserve((size_t)(e - a) * 320);
       for (uint32_t i = a; i < e; ++i) {

@@ -50,7 +50,7 @@ EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_inde
            "gwa_index_build_codes", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
            "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
            "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
-           "gwa_batch_read_counters"]
+           "gwa_batch_read_counters", "gwa_batch_results_range"]
 
 
 def lib():
@@ -81,6 +81,7 @@ def lib():
         L.gwa_batch_results.argtypes = [V, P(_Results)]
         L.gwa_batch_free.argtypes = [V]
         L.gwa_batch_read_counters.argtypes = [V, V]
+        L.gwa_batch_results_range.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, P(_Results)]
         _lib = L
     return _lib
 
@@ -263,13 +264,32 @@ class BidirectionalSuffixFilter:
             reporter(line)
 
 
+def reads_from_blobs(name_blob, name_off, seq_blob, seq_off, qual_blob=None, qual_off=None):
+    """A gwa_reads_t over caller-built blobs (used for large synthetic batches)."""
+    r = _Reads()
+    r.n = len(name_off) - 1
+    r.name = ctypes.cast(ctypes.c_char_p(name_blob), ctypes.c_void_p)
+    r.seq = ctypes.cast(ctypes.c_char_p(seq_blob), ctypes.c_void_p)
+    r.name_off, r.seq_off = name_off.ctypes.data, seq_off.ctypes.data
+    if qual_blob is not None:
+        r.qual, r.qual_off = ctypes.cast(ctypes.c_char_p(qual_blob), ctypes.c_void_p), qual_off.ctypes.data
+    else:
+        r.qual, r.qual_off = None, None
+    return r
+
+
 class Batch:
     """Split form for benchmarking: reads resident in HBM, run() = the timed kernels."""
 
-    def __init__(self, fmIndex, config, reads):
+    def __init__(self, fmIndex, config, reads=None, blobs=None):
         self._keep = []
-        r = _reads_struct(reads, self._keep)
-        self.n = len(reads)
+        if blobs is not None:
+            self._keep.append(blobs)
+            r = reads_from_blobs(*blobs)
+            self.n = r.n
+        else:
+            r = _reads_struct(reads, self._keep)
+            self.n = len(reads)
         self.h = ctypes.c_void_p()
         c = config._c()
         _check(lib().gwa_batch_create(fmIndex.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(self.h)))
@@ -282,9 +302,12 @@ class Batch:
         _check(lib().gwa_batch_stats(self.h, ctypes.byref(st)))
         return st
 
-    def results(self):
+    def results(self, first=0, count=None):
         res = _Results()
-        _check(lib().gwa_batch_results(self.h, ctypes.byref(res)))
+        if count is None:
+            _check(lib().gwa_batch_results(self.h, ctypes.byref(res)))
+        else:
+            _check(lib().gwa_batch_results_range(self.h, first, count, ctypes.byref(res)))
         return _take_results(res)
 
     def read_counters(self):

@@ -100,6 +100,8 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
 int gwa_batch_run(gwa_batch_t *b);
 int gwa_batch_stats(const gwa_batch_t *b, gwa_batch_stats_t *st);
 int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out);
+/* SAM for reads [first, first+count) only (n_reads = count). */
+int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out);
 void gwa_batch_free(gwa_batch_t *b);
 /* Instrumentation: per-read counters after gwa_batch_run, 12 int32 per read:
  * status, fm_searches, quick_steps, quickscan_blocks, search_blocks, states, sa_reads, n_hits,

@@ -109,8 +109,8 @@ class Index:
         codes = np.ascontiguousarray(codes, dtype=np.uint8)
         lengths = np.ascontiguousarray(lengths, dtype=np.int64)
         arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
-        f = np.ascontiguousarray(sa_f, dtype=np.int64) if sa_f is not None else None
-        r = np.ascontiguousarray(sa_r, dtype=np.int64) if sa_r is not None else None
+        f = np.ascontiguousarray(sa_f, dtype=np.uint32) if sa_f is not None else None
+        r = np.ascontiguousarray(sa_r, dtype=np.uint32) if sa_r is not None else None
         h = lib().orc_index_from_arrays(codes.ctypes.data, len(codes), len(names), ctypes.cast(arr, ctypes.c_void_p),
                                         lengths.ctypes.data, f.ctypes.data if f is not None else None,
                                         r.ctypes.data if r is not None else None)

@@ -35,52 +35,70 @@ def genome(contigs, config_id=1, scale=1.0):
 def reads(codes, lengths, n, m=100, max_subs=2, config_id=2, shard=0, indels=False, max_edits=5):
     """-> (seqs uint8 [n, m] codes, names list) ; substitutions: #subs uniform {0..max_subs},
     distinct positions, base uniform over the other 3."""
+    seqs = reads_codes(codes, lengths, n, m, max_subs, config_id, shard, indels, max_edits)
+    return seqs, ["r%09d" % i for i in range(n)]
+
+
+def reads_codes(codes, lengths, n, m=100, max_subs=2, config_id=2, shard=0, indels=False, max_edits=5,
+                chunk=1 << 20):
+    """Chunked generator core: -> uint8 [n, m] read codes."""
     rng = np.random.Generator(np.random.PCG64((SEED0 ^ config_id) + shard))
     N = len(codes)
-    offs = np.concatenate([[0], np.cumsum(lengths)])
-    # sample contig proportional to length, then start inside it
+    offs = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
     L = np.array(lengths, dtype=np.int64)
-    okc = L >= m + 2
-    p = np.where(okc, L - m - 1, 0).astype(np.float64)
+    p = np.where(L >= m + 2, L - m - 1, 0).astype(np.float64)
     p /= p.sum()
-    ci = rng.choice(len(L), size=n, p=p)
-    starts = offs[ci] + (rng.random(n) * (L[ci] - m - 1)).astype(np.int64)
-    idx = starts[:, None] + np.arange(m + 8)[None, :]
-    idx = np.minimum(idx, N - 1)
-    win = codes[idx]
-    out = win[:, :m].copy()
-    if not indels:
-        nsub = rng.integers(0, max_subs + 1, n)
-        for j in range(max_subs):
-            sel = nsub > j
-            pos = rng.integers(0, m, n)
-            # distinct positions: resample collisions with earlier ones is rare; shift instead
-            if j > 0:
-                pos = np.where(sel & (pos == prev), (pos + 1) % m, pos)
-            prev = pos if j == 0 else prev
-            r = rng.integers(1, 4, n).astype(np.uint8)
-            rows = np.nonzero(sel)[0]
-            out[rows, pos[rows]] = (out[rows, pos[rows]] + r[rows]) % 4
-    else:
-        out = np.empty((n, m), dtype=np.uint8)
-        ne = rng.integers(0, max_edits + 1, n)
-        for i in range(n):
-            s = list(win[i])
-            for _ in range(ne[i]):
-                t = rng.random()
-                p_ = int(rng.integers(5, m - 5))
-                if t < 0.6:
-                    s[p_] = (s[p_] + int(rng.integers(1, 4))) % 4
-                elif t < 0.8:
-                    s.insert(p_, int(rng.integers(0, 4)))
+    out = np.empty((n, m), dtype=np.uint8)
+    for c0 in range(0, n, chunk):
+        c = min(chunk, n - c0)
+        ci = rng.choice(len(L), size=c, p=p)
+        starts = offs[ci] + (rng.random(c) * (L[ci] - m - 1)).astype(np.int64)
+        if not indels:
+            idx = starts[:, None] + np.arange(m)[None, :]
+            blk = codes[np.minimum(idx, N - 1)]
+            nsub = rng.integers(0, max_subs + 1, c)
+            prev = None
+            for j in range(max_subs):
+                sel = nsub > j
+                pos = rng.integers(0, m, c)
+                if prev is not None:
+                    pos = np.where(sel & (pos == prev), (pos + 1) % m, pos)
                 else:
-                    del s[p_]
-            out[i] = np.array((s + [0] * m)[:m], dtype=np.uint8)
-    strand = rng.integers(0, 2, n)
-    rc = COMP[out[:, ::-1]]
-    out = np.where(strand[:, None] == 1, rc, out)
-    names = ["r%09d" % i for i in range(n)]
-    return out, names
+                    prev = pos
+                r = rng.integers(1, 4, c).astype(np.uint8)
+                rows = np.nonzero(sel)[0]
+                blk[rows, pos[rows]] = (blk[rows, pos[rows]] + r[rows]) % 4
+        else:
+            idx = starts[:, None] + np.arange(m + 8)[None, :]
+            win = codes[np.minimum(idx, N - 1)]
+            blk = np.empty((c, m), dtype=np.uint8)
+            ne = rng.integers(0, max_edits + 1, c)
+            for i in range(c):
+                s = list(win[i])
+                for _ in range(ne[i]):
+                    t = rng.random()
+                    p_ = int(rng.integers(5, m - 5))
+                    if t < 0.6:
+                        s[p_] = (s[p_] + int(rng.integers(1, 4))) % 4
+                    elif t < 0.8:
+                        s.insert(p_, int(rng.integers(0, 4)))
+                    else:
+                        del s[p_]
+                blk[i] = np.array((s + [0] * m)[:m], dtype=np.uint8)
+        strand = rng.integers(0, 2, c)
+        rc = COMP[blk[:, ::-1]]
+        out[c0:c0 + c] = np.where(strand[:, None] == 1, rc, blk)
+    return out
+
+
+def name_blob(n, start=0):
+    """names r%09d as one bytes blob + offsets (10 bytes each)."""
+    ids = np.arange(start, start + n, dtype=np.int64)
+    digits = np.empty((n, 10), dtype=np.uint8)
+    digits[:, 0] = ord("r")
+    for d in range(9):
+        digits[:, 9 - d] = ord("0") + (ids // (10 ** d)) % 10
+    return digits.tobytes(), np.arange(0, 10 * (n + 1), 10, dtype=np.uint64)
 
 
 def to_strings(seqs):
