@@ -20,6 +20,24 @@ GWA_HD int64_t jshl(int64_t x, int64_t s) { return (int64_t)((uint64_t)x << (s &
 GWA_HD int64_t jushr(int64_t x, int64_t s) { return (int64_t)((uint64_t)x >> (s & 63)); }
 GWA_HD int popc64(uint64_t x) { return __builtin_popcountll(x); }
 
+// a[i] for a runtime i through unrolled selects: small arrays stay in VGPRs instead of scratch
+// (the empty asm pins each element as a VGPR value, so the select chain is not folded back into
+// a load from a runtime address, which would force the array into scratch memory)
+template <class T>
+GWA_HD T pinv(T x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
+template <class T, int N>
+GWA_HD T pick(const T (&a)[N], int i) {
+  T v = pinv(a[0]);
+#pragma unroll
+  for (int j = 1; j < N; ++j) v = (i == j) ? pinv(a[j]) : v;
+  return v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Rank on one 64-B Occ block (A/OccurrenceCountTable.java:80-107, A/ACGTSequence.java:456-549)
 // ---------------------------------------------------------------------------------------------
@@ -118,7 +136,7 @@ struct Caps {
 template <int R>
 struct LaneMem {
   DState<R> *arena;
-  int32_t *heap;
+  uint64_t *heap;  // PriorityQueue array of (key << 16 | state index); key cached, refreshed on mutation
   DHit *hits;
   int32_t *list;
   uint16_t *cigar;
@@ -131,7 +149,7 @@ template <int R>
 GWA_HD size_t laneBytes(const Caps &c) {
   size_t b = 0;
   b += sizeof(DState<R>) * (size_t)c.arena;
-  b += 4 * (size_t)c.heap;
+  b += 8 * (size_t)c.heap;
   b += sizeof(DHit) * (size_t)c.hits;
   b += 4 * (size_t)c.list;
   b += 2 * (size_t)c.cigar;
@@ -147,7 +165,7 @@ GWA_HD LaneMem<R> laneMem(uint8_t *base, const Caps &c) {
   LaneMem<R> L;
   size_t b = 0;
   L.arena = (DState<R> *)(base + b); b += sizeof(DState<R>) * (size_t)c.arena;
-  L.heap = (int32_t *)(base + b); b += 4 * (size_t)c.heap;
+  L.heap = (uint64_t *)(base + b); b += 8 * (size_t)c.heap;
   L.hits = (DHit *)(base + b); b += sizeof(DHit) * (size_t)c.hits;
   L.list = (int32_t *)(base + b); b += 4 * (size_t)c.list;
   L.cigar = (uint16_t *)(base + b); b += 2 * (size_t)c.cigar;
@@ -237,48 +255,84 @@ struct BsfLane {
     return 0;
   }
 
-  // ---- QueryMask (A/QueryMask.java:41-97) ----
-  GWA_HD uint64_t &mask(int strand, int fr, int ch, int b) { return L.masks[((strand * 2 + fr) * 4 + ch) * 4 + b]; }
+  // ---- QueryMask (A/QueryMask.java:41-97), computed on the fly ----
+  // The read (after replaceN_withA) is kept 2-bit packed in registers for both strands:
+  // qw[s][w] holds positions 32w..32w+31.  A 64-bit pattern window is a funnel shift of three
+  // words, a 2-bit compare and an even-bit compress (no per-read mask arrays in memory).
+  uint64_t qw[2][8];
   GWA_HD void buildMasks() {
-    const int nb = (m + 63) / 64;
-    for (int s = 0; s < 2; ++s)
-      for (int fr = 0; fr < 2; ++fr)
-        for (int c = 0; c < 4; ++c)
-          for (int b = 0; b < 4; ++b) mask(s, fr, c, b) = 0;
-    for (int s = 0; s < 2; ++s)
-      for (int i = 0; i < m; ++i) {
-        int c = q(s, i);
-        mask(s, 0, c, i >> 6) |= 1ULL << (i & 63);
-        int j = m - i - 1;
-        mask(s, 1, c, j >> 6) |= 1ULL << (j & 63);
+    for (int s2 = 0; s2 < 2; ++s2)
+      for (int w = 0; w < 8; ++w) qw[s2][w] = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      uint64_t v0 = 0, v1 = 0;
+      for (int j = 0; j < 32; ++j) {
+        const int i = w * 32 + j;
+        if (i < m) {
+          v0 |= (uint64_t)q(0, i) << (2 * j);
+          v1 |= (uint64_t)q(1, i) << (2 * j);
+        }
       }
-    (void)nb;
+      qw[0][w] = v0;
+      qw[1][w] = v1;
+    }
   }
-  // BitVector.substring64 (A/BitVector.java:106-116) on a pattern mask of m bits
-  GWA_HD int64_t substring64(int strand, int fr, int ch, int64_t start, int64_t end) {
-    const int nb = (m + 63) / 64;
-    int pos = (int)(start / 64);
-    if (pos >= nb) return 0;
-    int64_t range = end - start;
-    int64_t msk = (range >= 64) ? ~0LL : ~jshl(~0LL, range);
-    int64_t offset = start % 64;
-    int64_t low = jushr((int64_t)mask(strand, fr, ch, pos), offset);
-    int64_t high = pos + 1 < nb ? jshl((int64_t)mask(strand, fr, ch, pos + 1) & ~jshl(~0LL, offset), 64 - offset) : 0;
-    return (high | low) & msk;
+  GWA_HD uint64_t qword(int strand, int w) const {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = (w == i) ? (strand ? qw[1][i] : qw[0][i]) : v;
+    return v;
   }
+  GWA_HD static uint64_t compressEven(uint64_t x) {
+    x &= 0x5555555555555555ULL;
+    x = (x | (x >> 1)) & 0x3333333333333333ULL;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0FULL;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFULL;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFULL;
+    x = (x | (x >> 16)) & 0x00000000FFFFFFFFULL;
+    return x;
+  }
+  GWA_HD static uint64_t bitrev64(uint64_t x) {
+#if defined(__clang__)
+    return __builtin_bitreverse64(x);
+#else
+    x = ((x >> 1) & 0x5555555555555555ULL) | ((x & 0x5555555555555555ULL) << 1);
+    x = ((x >> 2) & 0x3333333333333333ULL) | ((x & 0x3333333333333333ULL) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0FULL) | ((x & 0x0F0F0F0F0F0F0F0FULL) << 4);
+    x = ((x >> 8) & 0x00FF00FF00FF00FFULL) | ((x & 0x00FF00FF00FF00FFULL) << 8);
+    x = ((x >> 16) & 0x0000FFFF0000FFFFULL) | ((x & 0x0000FFFF0000FFFFULL) << 16);
+    return (x >> 32) | (x << 32);
+#endif
+  }
+  // bit j = (q[strand][start + j] == ch) for start + j < m, else 0   (start >= 0)
+  GWA_HD uint64_t eqWindow(int strand, int ch, int start) const {
+    if (start >= m) return 0;
+    const int w = start >> 5, sh = 2 * (start & 31);
+    const uint64_t a = qword(strand, w), b = qword(strand, w + 1), c = qword(strand, w + 2);
+    const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a;
+    const uint64_t hi = sh ? (b >> sh) | (c << (64 - sh)) : b;
+    const uint64_t pat = 0x5555555555555555ULL * (uint64_t)ch;
+    const uint64_t xl = lo ^ pat, xh = hi ^ pat;
+    uint64_t r = compressEven(~(xl | (xl >> 1))) | (compressEven(~(xh | (xh >> 1))) << 32);
+    const int range = m - start;
+    if (range < 64) r &= (1ULL << range) - 1ULL;
+    return r;
+  }
+  // QueryMask.getBidirectionalPatternMask64 (A/QueryMask.java:73-97): forward = patternMaskF window,
+  // backward = patternMaskR window = the reversed forward window ending at the pivot.
   GWA_HD int64_t patternMask64(int strand, bool isForward, int nextIdx, int pivot, int cursor, int ch, int margin) {
     int64_t p;
     if (isForward) {
       int pos = nextIdx - margin;
-      if (pos < 0) {
-        p = substring64(strand, 0, ch, 0, 64);
-        p = jshl(p, -pos);
-      } else
-        p = substring64(strand, 0, ch, pos, m);
+      if (pos < 0) p = jshl((int64_t)eqWindow(strand, ch, 0), -pos);
+      else p = (int64_t)eqWindow(strand, ch, pos);
     } else {
-      int b = m - pivot;
+      uint64_t f;
+      if (pivot <= 0) f = 0;
+      else if (pivot >= 64) f = bitrev64(eqWindow(strand, ch, pivot - 64));
+      else f = bitrev64((eqWindow(strand, ch, 0) & ((1ULL << pivot) - 1ULL)) << (64 - pivot));
+      p = (int64_t)f;
       int rshift = pivot - cursor - margin;
-      p = substring64(strand, 1, ch, b, b + 64);
       if (rshift >= 0) p = jushr(p, rshift);
       else p = jshl(p, -rshift);
     }
@@ -319,30 +373,33 @@ struct BsfLane {
   GWA_HD static bool siGetF(const DState<R> &s, int ch, uint32_t *lb, uint32_t *ub) {
     uint8_t t = siType(s);
     if (!siValid(s) || (t != SI_FWD && t != SI_BID)) return false;
-    if (s.lb[ch] >= s.ub[ch]) return false;
-    *lb = s.lb[ch]; *ub = s.ub[ch];
+    const uint32_t l = pick(s.lb, ch), u = pick(s.ub, ch);
+    if (l >= u) return false;
+    *lb = l; *ub = u;
     return true;
   }
   GWA_HD static bool siGetB(const DState<R> &s, int ch, uint32_t *lb, uint32_t *ub) {
     uint8_t t = siType(s);
     if (!siValid(s)) return false;
+    const uint32_t l = pick(s.lb, ch), u = pick(s.ub, ch);
     if (t == SI_BWD) {
-      if (s.lb[ch] >= s.ub[ch]) return false;
-      *lb = s.lb[ch]; *ub = s.ub[ch];
+      if (l >= u) return false;
+      *lb = l; *ub = u;
       return true;
     }
     if (t != SI_BID) return false;
-    if (s.lb[ch] >= s.ub[ch]) return false;
+    if (l >= u) return false;
     uint32_t x = 0;
-    for (int j = 0; j < ch; ++j) x += s.ub[j] - s.lb[j];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x += j < ch ? s.ub[j] - s.lb[j] : 0u;
     *lb = s.bBase + x;
-    *ub = s.bBase + x + (s.ub[ch] - s.lb[ch]);
+    *ub = s.bBase + x + (u - l);
     return true;
   }
   GWA_HD static bool siIsEmpty(const DState<R> &s, int ch) {
     if (!siValid(s)) return true;  // NullPointerException in the reference; never reached (clipped tails)
     if (siType(s) == SI_EMPTY) return true;
-    return s.lb[ch] >= s.ub[ch];
+    return pick(s.lb, ch) >= pick(s.ub, ch);
   }
   GWA_HD void siInit(DState<R> &d, int dir) {  // FMIndexOnGenome.initSet (:117-128)
     d.meta = (uint8_t)((d.meta & ~3) | M_SIVALID | (dir == D_FORWARD ? SI_FWD : dir == D_BACKWARD ? SI_BWD : SI_BID));
@@ -356,7 +413,11 @@ struct BsfLane {
   // ---- state flags ----
   GWA_HD DState<R> &S(int i) { return L.arena[i]; }
   GWA_HD int minK(int s) { return (int)(((uint32_t)S(s).state >> 8) & 0xFF); }
-  GWA_HD void setMinK(int s, int d) { S(s).state &= ~(0xFF << 8); S(s).state |= (d & 0xFF) << 8; }
+  GWA_HD void setMinK(int s, int d) {
+    invalidateCache();
+    S(s).state &= ~(0xFF << 8);
+    S(s).state |= (d & 0xFF) << 8;
+  }
   GWA_HD int prio(int s) { return (int)(((uint32_t)S(s).state >> 16) & 0xFF); }
   GWA_HD bool hasHit(int s) { return (((uint32_t)S(s).state >> 24) & 1) != 0; }
   GWA_HD bool isClipped(int s) { return (((uint32_t)S(s).state >> 25) & 1) != 0; }
@@ -410,46 +471,68 @@ struct BsfLane {
     }
     return sum;
   }
-  // StateQueue comparator (:141-150)
-  GWA_HD int compare(int a, int b) {
-    int diff = prio(a) - prio(b);
-    if (diff == 0) diff = -(chainScore(a, false) - chainScore(b, false));
-    if (diff == 0) diff = -(cProcessed(S(a)) - cProcessed(S(b)));
-    return diff;
+  // StateQueue comparator (:141-150) as a cached sortable key: priority asc, score() desc,
+  // processed bases desc.  Keys are live in the reference; the only mutations that change them
+  // (SearchState.update splicing a chain, setLowerBoundOfK) call refreshKeys().
+  GWA_HD uint64_t keyOf(int s) {
+    if (s == cacheIdx && cache.nextSplit < 0) {
+      const int sc0 = stateScore(cache, 0, false);
+      const uint64_t sp0 = (uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc0) & 0xFFFFFFFFULL;
+      return ((uint64_t)(((uint32_t)cache.state >> 16) & 0xFF) << 40) | (sp0 << 8) | (uint64_t)(255 - cProcessed(cache));
+    }
+    const int sc = chainScore(s, false);
+    const uint64_t sp = (uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc) & 0xFFFFFFFFULL;
+    const int pr = prio(s);
+    const int proc = cProcessed(S(s));
+    return ((uint64_t)pr << 40) | (sp << 8) | (uint64_t)(255 - proc);
   }
-  // java.util.PriorityQueue.offer / poll
-  GWA_HD void queueAdd(int e) {
-    if (e < 0) return;
+  GWA_HD void refreshKeys() {
+    for (int i = 0; i < heapSize; ++i) {
+      const int idx = (int)(L.heap[i] & 0xFFFF);
+      L.heap[i] = (keyOf(idx) << 16) | (uint64_t)idx;
+    }
+  }
+  // java.util.PriorityQueue.offer / poll on cached keys
+  GWA_HD void queueAddKeyed(uint64_t e) {
     if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
     int kk = heapSize++;
+    const uint64_t ek = e >> 16;
     while (kk > 0) {
       int parent = (kk - 1) >> 1;
-      int p = L.heap[parent];
-      if (compare(e, p) >= 0) break;
+      uint64_t p = L.heap[parent];
+      if (ek >= (p >> 16)) break;
       L.heap[kk] = p;
       kk = parent;
     }
     L.heap[kk] = e;
   }
+  GWA_HD void queueAdd(int e) {
+    if (e < 0) return;
+    queueAddKeyed((keyOf(e) << 16) | (uint64_t)e);
+  }
   GWA_HD int queuePoll() {
     if (heapSize == 0) return -1;
     int s = --heapSize;
-    int result = L.heap[0];
-    int x = L.heap[s];
+    const uint64_t result = L.heap[0];
+    const uint64_t x = L.heap[s];
     if (s != 0) {
       int kk = 0, half = heapSize >> 1;
+      const uint64_t xk = x >> 16;
       while (kk < half) {
         int child = (kk << 1) + 1;
-        int c = L.heap[child];
+        uint64_t c = L.heap[child];
         int right = child + 1;
-        if (right < heapSize && compare(c, L.heap[right]) > 0) c = L.heap[child = right];
-        if (compare(x, c) <= 0) break;
+        if (right < heapSize) {
+          uint64_t rc = L.heap[right];
+          if ((c >> 16) > (rc >> 16)) { c = rc; child = right; }
+        }
+        if (xk <= (c >> 16)) break;
         L.heap[kk] = c;
         kk = child;
       }
       L.heap[kk] = x;
     }
-    return result;
+    return (int)(result & 0xFFFF);
   }
 
   // ---- FMQuickScan.scanMismatchLocations (S/FMQuickScan.java:66-94) ----
@@ -606,6 +689,28 @@ struct BsfLane {
     return (int)((ix.text2[p >> 5] >> ((p & 31) * 2)) & 3);
   }
   // returns 0 ok, 1 null (no alignment), <0 overflow
+  // DP query code p of the fragment q[strand][qs,qe) (reversed on strand 1, :532-534)
+  GWA_HD int dpQ(int strand, int qs, int qe, int p) const { return strand == 1 ? qcode(strand, qe - 1 - p) : qcode(strand, qs + p); }
+
+  // One Myers/Hyyro block step (A/BitParallelSmithWaterman.java:476-504); vp/vn in/out
+  GWA_HD static int dpBlock(uint64_t x, int hin, uint64_t &vp, uint64_t &vn) {
+    if (hin < 0) x |= 1ULL;
+    const uint64_t d0 = (((x & vp) + vp) ^ vp) | x | vn;
+    const uint64_t hp = vn | ~(d0 | vp);
+    const uint64_t hn = d0 & vp;
+    const int hout = (int)((hp >> 63) & 1ULL) - (int)((hn >> 63) & 1ULL);
+    uint64_t hp2 = hp << 1, hn2 = hn << 1;
+    if (hin < 0) hn2 |= 1ULL;
+    if (hin > 0) hp2 |= 1ULL;
+    vp = hn2 | ~(d0 | hp2);
+    vn = d0 & hp2;
+    return hout;
+  }
+
+  // BitParallelSmithWaterman.alignBlockDetailed (A/BitParallelSmithWaterman.java:141-147,394-644).
+  // The live column (<=4 blocks of 64 rows) stays in VGPRs; the vp/vn history the traceback needs
+  // is written to HBM scratch, with one byte per column recording which cells were written
+  // (cells never written read as 0, as the reference's zero-initialised long[][] do).
   GWA_HD int alignBlockDetailed(int strand, int qs, int qe, int64_t refStart, int64_t refEnd, int *outPos, int *outDiff,
                                 int *cigOff, int *cigLen) {
     const int w = 64;
@@ -613,63 +718,84 @@ struct BsfLane {
     const int kb = cfg.bandWidth;
     const int bMax = mq + w - 1 >= w ? (mq + w - 1) / w : 1;
     const int N = (int)(refEnd - refStart);
-    if (bMax > 4 || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || mq + N + 2 > caps.path) { status = ST_OVERFLOW; return -1; }
-    auto qcode = [&](int p) -> int { return strand == 1 ? q(strand, qe - 1 - p) : q(strand, qs + p); };
-    uint64_t peq[4][4];
-    for (int c = 0; c < 4; ++c)
-      for (int b = 0; b < 4; ++b) peq[c][b] = 0;
-    for (int p = 0; p < mq; ++p) peq[qcode(p)][p >> 6] |= 1ULL << (p & 63);
-    uint64_t *vp = L.dp;
-    uint64_t *vn = L.dp + (size_t)bMax * (N + 1);
-    auto VP = [&](int r, int j) -> uint64_t & { return vp[(size_t)r * (N + 1) + j]; };
-    auto VN = [&](int r, int j) -> uint64_t & { return vn[(size_t)r * (N + 1) + j]; };
-    for (int r = 0; r < bMax; ++r)
-      for (int j = 0; j <= N; ++j) { VP(r, j) = 0; VN(r, j) = 0; }
-    for (int r = 0; r < bMax; ++r) { VP(r, 0) = ~0ULL; VN(r, 0) = 0; }
-    int D[4] = {0, 0, 0, 0};
+    if (bMax > 4 || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || mq + 2 * N + 4 > caps.path) { status = ST_OVERFLOW; return -1; }
+    uint64_t pA[4] = {0, 0, 0, 0}, pC[4] = {0, 0, 0, 0}, pG[4] = {0, 0, 0, 0}, pT[4] = {0, 0, 0, 0};
+    for (int p = 0; p < mq; ++p) {
+      const int c = dpQ(strand, qs, qe, p);
+      const uint64_t bit = 1ULL << (p & 63);
+      const int b = p >> 6;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r == b) {
+          if (c == 0) pA[r] |= bit;
+          else if (c == 1) pC[r] |= bit;
+          else if (c == 2) pG[r] |= bit;
+          else pT[r] |= bit;
+        }
+      }
+    }
+    uint64_t *hvp = L.dp;                         // [col 1..N][block] history
+    uint64_t *hvn = L.dp + (size_t)bMax * (N + 1);
+    uint8_t *wr = L.path + mq + N + 2;            // per column: bits 0-3 computed, bits 4-7 activated-as-input
+    for (int j = 0; j <= N; ++j) wr[j] = 0;
+    uint64_t vp[4], vn[4];
+    int D[4] = {0, 0, 0, 0}, sb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      vp[r] = ~0ULL;
+      vn[r] = 0;
+      const int v = mq - ((r + 1) * w) + kb;
+      sb[r] = v > 0 ? v : 0;
+    }
+    wr[0] = (uint8_t)(((1 << bMax) - 1) << 4);  // column 0 inputs: ~0 / 0 for every block
     D[0] = mq;
-    int scoreBoundary[4];
-    for (int i = 0; i < bMax; ++i) { int v = mq - ((i + 1) * w) + kb; scoreBoundary[i] = v > 0 ? v : 0; }
     int bCeil = (kb + w - 1) / w;
     if (bCeil < 1) bCeil = 1;
     int have = 0;  // int, not bool: see quickScan
     int bestTail = 0, bestDiff = 0;
-    auto alignBlock = [&](int j, int ch, int r, int hin) -> int {
-      uint64_t vpv = VP(r, j), vnv = VN(r, j);
-      uint64_t x = ch < 4 ? peq[ch][r] : 0ULL;
-      if (hin < 0) x |= 1ULL;
-      uint64_t d0 = (((x & vpv) + vpv) ^ vpv) | x | vnv;
-      uint64_t hp = vnv | ~(d0 | vpv);
-      uint64_t hn = d0 & vpv;
-      int hout = (int)((hp >> 63) & 1ULL) - (int)((hn >> 63) & 1ULL);
-      uint64_t hp2 = hp << 1, hn2 = hn << 1;
-      if (hin < 0) hn2 |= 1ULL;
-      if (hin > 0) hp2 |= 1ULL;
-      VP(r, j + 1) = hn2 | ~(d0 | hp2);
-      VN(r, j + 1) = d0 & hp2;
-      return hout;
-    };
     for (int j = 0; j < N; ++j) {
-      int ch = refCode(refStart + j);
+      const int ch = refCode(refStart + j);
       int carry = 0;
-      for (int b = 0; b < bCeil; ++b) {
-        int ns = alignBlock(j, ch, b, carry);
-        D[b] += ns;
-        carry = ns;
+      uint8_t wmask = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r < bCeil) {
+          const uint64_t x = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
+          const int ns = dpBlock(x, carry, vp[r], vn[r]);
+          D[r] += ns;
+          carry = ns;
+          hvp[(size_t)(j + 1) * bMax + r] = vp[r];
+          hvn[(size_t)(j + 1) * bMax + r] = vn[r];
+          wmask |= (uint8_t)(1 << r);
+        }
       }
-      if (bCeil < bMax && D[bCeil - 1] - carry <= scoreBoundary[bCeil - 1] &&
-          ((ch < 4 && (peq[ch][bCeil] & 1ULL) != 0ULL) || carry < 0)) {
-        VP(bCeil, j) = ~0ULL;
-        VN(bCeil, j) = 0ULL;
-        int ns = alignBlock(j, ch, bCeil, carry);
-        D[bCeil] = D[bCeil - 1] - carry + ns;
+      const int dPrev = pick(D, bCeil - 1);
+      const uint64_t nextPeq = ch == 0 ? pick(pA, bCeil) : ch == 1 ? pick(pC, bCeil) : ch == 2 ? pick(pG, bCeil) : ch == 3 ? pick(pT, bCeil) : 0ULL;
+      if (bCeil < bMax && dPrev - carry <= pick(sb, bCeil - 1) && (((nextPeq & 1ULL) != 0ULL) || carry < 0)) {
+        // activate block bCeil with input column j = ~0 / 0 (:427-428)
+        wr[j] |= (uint8_t)(1 << (4 + bCeil));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (r == bCeil) {
+            vp[r] = ~0ULL;
+            vn[r] = 0ULL;
+            const uint64_t x = nextPeq;
+            const int ns = dpBlock(x, carry, vp[r], vn[r]);
+            D[r] = dPrev - carry + ns;
+            hvp[(size_t)(j + 1) * bMax + r] = vp[r];
+            hvn[(size_t)(j + 1) * bMax + r] = vn[r];
+            wmask |= (uint8_t)(1 << r);
+          }
+        }
         bCeil++;
       } else {
-        while (bCeil > 1 && D[bCeil - 1] > scoreBoundary[bCeil - 1] + w) --bCeil;
+        while (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
       }
+      wr[j + 1] |= wmask;
       if (bCeil == bMax) {
-        if (!have) { have = 1; bestTail = j; bestDiff = D[bCeil - 1]; continue; }
-        if (bestDiff > D[bCeil - 1]) { bestTail = j; bestDiff = D[bCeil - 1]; }
+        const int dl = pick(D, bCeil - 1);
+        if (!have) { have = 1; bestTail = j; bestDiff = dl; continue; }
+        if (bestDiff > dl) { bestTail = j; bestDiff = dl; }
       }
     }
     (void)bestDiff;
@@ -682,10 +808,20 @@ struct BsfLane {
     for (;;) {
       int pth = 0;  // 0 NONE 1 DIAG 2 DIAG_MM 3 LEFT 4 UP
       if (col >= 0 && row >= 0) {
-        int block = row / w, offset = row % w;
-        uint64_t vpf = VP(block, col + 1) & (1ULL << offset);
-        uint64_t vnf = VN(block, col + 1) & (1ULL << offset);
-        if (refCode(refStart + col) == qcode(row)) pth = 1;
+        const int block = row >> 6, offset = row & 63;
+        const uint8_t wb = wr[col + 1];
+        uint64_t vpw = 0, vnw = 0;
+        if ((wb >> block) & 1) {  // computed at column col (the later write when both happened)
+          vpw = hvp[(size_t)(col + 1) * bMax + block];
+          vnw = hvn[(size_t)(col + 1) * bMax + block];
+          if ((wb >> (4 + block)) & 1) { vpw = ~0ULL; vnw = 0; }
+        } else if ((wb >> (4 + block)) & 1) {
+          vpw = ~0ULL;
+          vnw = 0;
+        }
+        const uint64_t vpf = vpw & (1ULL << offset);
+        const uint64_t vnf = vnw & (1ULL << offset);
+        if (refCode(refStart + col) == dpQ(strand, qs, qe, row)) pth = 1;
         else if (vpf != 0) { pth = 4; diff++; }
         else if (vnf == 0) { pth = 2; diff++; }
         else { pth = 3; diff++; }
@@ -705,34 +841,37 @@ struct BsfLane {
     // cigarStr = reverse(path); leading/trailing S/I/D -> S, I/D subtract from diff
     int left = 0, right = 0;
     for (int i = 0; i < plen; ++i) {
-      char t = (char)path[plen - 1 - i];
+      const char t = (char)path[plen - 1 - i];
       if (t == 'S') left++;
       else if (t == 'I' || t == 'D') { left++; diff--; }
       else break;
     }
     for (int i = plen - 1; i >= left; --i) {
-      char t = (char)path[plen - 1 - i];
+      const char t = (char)path[plen - 1 - i];
       if (t == 'S') right++;
       else if (t == 'I' || t == 'D') { right++; diff--; }
       else break;
     }
     // CIGAR.add(char) over S^left + middle + S^right (A/CIGAR.java:143-156)
-    int off = nCigar;
-    int curT = -1, curL = 0;
-    auto push = [&](int t) {
-      if (t == curT) { curL++; return; }
-      if (curT >= 0 && putCigarOp(curT, curL) < 0) return;
-      curT = t;
-      curL = 1;
-    };
-    for (int i = 0; i < left; ++i) push(4);
+    const int off = nCigar;
+    int curT = 4, curL = left;
     for (int i = left; i < plen - right; ++i) {
-      char t = (char)path[plen - 1 - i];
-      push(t == 'M' ? 0 : t == 'I' ? 1 : t == 'D' ? 2 : 4);
+      const char t = (char)path[plen - 1 - i];
+      const int ty = t == 'M' ? 0 : t == 'I' ? 1 : t == 'D' ? 2 : 4;
+      if (ty == curT) { curL++; continue; }
+      if (curL > 0 && putCigarOp(curT, curL) < 0) return -1;
+      curT = ty;
+      curL = 1;
     }
-    for (int i = 0; i < right; ++i) push(4);
-    if (curT >= 0) putCigarOp(curT, curL);
-    if (status == ST_OVERFLOW) return -1;
+    if (right > 0) {
+      if (curT == 4) curL += right;
+      else {
+        if (curL > 0 && putCigarOp(curT, curL) < 0) return -1;
+        curT = 4;
+        curL = right;
+      }
+    }
+    if (curL > 0 && putCigarOp(curT, curL) < 0) return -1;
     *cigOff = off;
     *cigLen = nCigar - off;
     *outPos = leftMostPos;
@@ -791,6 +930,7 @@ struct BsfLane {
     int newK = hitTotalDiff(al);
     if (newK > k) return true;
     setMinK(c, newK);
+    refreshKeys();  // c may still be queued (duplicate references)
     int head = sortSplits(al);
     if (status == ST_ERROR || status == ST_OVERFLOW) return false;
     resultAdd(head);
@@ -799,7 +939,7 @@ struct BsfLane {
 
   // ---- ReadAlignmentNFA.nextState (S/ReadAlignmentNFA.java:127-203) ----
   // returns: -1 null, else (hasMatch, new rows/kOffset written into out)
-  GWA_HD bool nfaNext(const DState<R> &s, int ch, int strand, uint64_t *outRows, int *outH, int *outKOff, bool *hasMatch) {
+  GWA_HD bool nfaNext(const DState<R> &s, int ch, int strand, uint64_t (&outRows)[R], int *outH, int *outKOff, bool *hasMatch) {
     const int height = s.nrows;
     const int kOff = s.kOffset;
     const int kk = kOff + height - 1;
@@ -807,24 +947,39 @@ struct BsfLane {
     const int64_t qeq = patternMask64(strand, cFwd(s), cNextIdx(s), s.pivot, s.cursor, ch, kr);
     const int progress = cProcessed(s);
     const int frag = cFrag(s);
+    const int soff = progress - kk;
     int64_t next[R];
     int minKwithMatch = kk + 1, minKwithProgress = kk + 1;
-    next[0] = jshl((int64_t)s.nfa[0] & qeq, 1);
-    if (next[0] != 0) { minKwithMatch = 0; minKwithProgress = 0; }
-    next[0] &= stairMask(kOff, progress - kk);
-    for (int i = 1; i < height; ++i) {
-      next[i] = jshl((int64_t)s.nfa[i] & qeq, 1);
-      if (minKwithMatch > kk && next[i] != 0) minKwithMatch = i;
-      next[i] |= (int64_t)s.nfa[i - 1] | jshl((int64_t)s.nfa[i - 1], 1) | jshl(next[i - 1], 1);
-      next[i] &= stairMask(kOff + i, progress - kk);
-      if (minKwithProgress > kk && (next[i] & jshl(1, height)) != 0) minKwithProgress = i;
+    int64_t prevRow = 0, prevNext = 0;
+    // R'_0 = ((R_0 & P[ch]) << 1) & staircase;  R'_i = ((R_i & P[ch]) << 1) | R_{i-1} | R_{i-1} << 1 | R'_{i-1} << 1
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      next[i] = 0;
+      if (i < height) {
+        const int64_t a = (int64_t)s.nfa[i];
+        int64_t nx = jshl(a & qeq, 1);
+        if (i == 0) {
+          if (nx != 0) { minKwithMatch = 0; minKwithProgress = 0; }
+          nx &= stairMask(kOff, soff);
+        } else {
+          if (minKwithMatch > kk && nx != 0) minKwithMatch = i;
+          nx |= prevRow | jshl(prevRow, 1) | jshl(prevNext, 1);
+          nx &= stairMask(kOff + i, soff);
+          if (minKwithProgress > kk && (nx & jshl(1, height)) != 0) minKwithProgress = i;
+        }
+        next[i] = nx;
+        prevRow = a;
+        prevNext = nx;
+      }
     }
     const int mPos = kk + frag - progress;
     int rem = -1;
     int hm = 0;
     if (mPos < 64) {
-      for (int nm = 0; nm < height; ++nm)
-        if (rem < 0 && (next[nm] & jshl(1, mPos)) != 0) { rem = nm; hm = 1; }
+      const int64_t bit = jshl(1, mPos);
+#pragma unroll
+      for (int nm = 0; nm < R; ++nm)
+        if (nm < height && rem < 0 && (next[nm] & bit) != 0) { rem = nm; hm = 1; }
     }
     if (!hm) {
       int mk = minKwithMatch < minKwithProgress ? minKwithMatch : minKwithProgress;
@@ -833,11 +988,13 @@ struct BsfLane {
     }
     // removeLayersFromAutomaton (:205-215): the OLD rows when nothing is trimmed
     if (rem == 0) {
-      for (int i = 0; i < height; ++i) outRows[i] = s.nfa[i];
+#pragma unroll
+      for (int i = 0; i < R; ++i) outRows[i] = s.nfa[i];
       *outH = height;
     } else {
-      int nh = height - rem;
-      for (int h = 0; h < nh; ++h) outRows[h] = (uint64_t)jushr(next[h + rem], 1);
+      const int nh = height - rem;
+#pragma unroll
+      for (int h = 0; h < R; ++h) outRows[h] = h < nh ? (uint64_t)jushr(pick(next, h + rem), 1) : 0ULL;
       *outH = nh;
     }
     *outKOff = kOff + rem;
@@ -926,6 +1083,7 @@ struct BsfLane {
 
   // nextStateAfterSplit / nextStateAfterClipping (:803-838); -1 null, -2 overflow
   GWA_HD int nextStateAfterSplit(int c, bool clip) {
+    invalidateCache();
     updateSplitFlag(c);
     const int mk = minK(c);
     if (!(mk < k)) return -1;
@@ -994,12 +1152,14 @@ struct BsfLane {
   // SearchState.update (:861-875); -1 = null
   GWA_HD int update(int self, int oldS, int newS) {
     if (oldS == self) return newS;
+    invalidateCache();
     int prev = self;
     while (S(prev).nextSplit != oldS) {
       prev = S(prev).nextSplit;
       if (prev < 0) return -1;
     }
     S(prev).nextSplit = newS;
+    refreshKeys();  // score() of every chain through prev changed
     return self;
   }
 
@@ -1071,58 +1231,61 @@ struct BsfLane {
     while (heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR) {
       if (numFMIndexSearches > upper) break;
       const int base = queuePoll();
+      // the polled state and its split chain are read once into registers
+      DState<R> B;
+      loadState(base, B);
+      tr(1, (uint32_t)base, curWord(B), (uint32_t)B.state);
       int c = base;
-      tr(1, (uint32_t)base, curWord(S(base)), (uint32_t)S(base).state);
+      DState<R> C = B;
       {
-        int nx = c;
         int reported = 0;
-        while (hasHit(nx) || isClipped(nx) || cRemaining(S(nx)) == 0) {
-          if (S(nx).nextSplit < 0) {
-            if (!reportAlignment(c)) return;
+        while (((((uint32_t)C.state >> 24) & 3) != 0) || cRemaining(C) == 0) {  // hasHit | isClipped | done
+          if (C.nextSplit < 0) {
+            if (!reportAlignment(base)) return;
             reported = 1;
             break;
           }
-          nx = S(nx).nextSplit;
+          c = C.nextSplit;
+          loadState(c, C);
         }
         if (reported) continue;
-        c = nx;
       }
-      if (isFinished(c)) continue;
-      const int nm = minK(c);
+      if ((C.state & 0x1F) == 0x1F) continue;  // isFinished
+      const int nm = (int)(((uint32_t)C.state >> 8) & 0xFF);
       if (nm > minMismatches) continue;
       if (minMismatches - nm < 0) continue;
       {
-        int ub = chainScore(base, true);
+        const int ub = B.nextSplit < 0 ? stateScore(B, 0, true) : chainScore(base, true);
         if (ub < 0 || ub < bestScore) continue;
       }
-      const int strand = cStrand(S(c));
-      const int nextBase = q(strand, cNextIdx(S(c)));
+      const int strand = cStrand(C);
+      const int nextBase = qcode(strand, cNextIdx(C));
       int advanced = 0;
-      {
-        int ch = nextBase;
-        if (!isChecked(c, ch)) {
-          updateFlag(c, ch);
-          if (!siIsEmpty(S(c), ch)) {
-            int ns = nextState(c, ch);
-            if (ns == -2) return;
-            if (ns >= 0) { queueAdd(update(base, c, ns)); advanced = 1; }
-          }
+      if (!(C.state & (1 << nextBase))) {
+        C.state |= 1 << nextBase;  // updateFlag
+        storeStateWord(c, C.state);
+        if (!siIsEmpty(C, nextBase)) {
+          const int ns = nextStateLocal(c, C, nextBase);
+          if (ns == -2) return;
+          if (ns >= 0) { queueAdd(update(base, c, ns)); advanced = 1; }
         }
       }
       if (advanced) continue;
       for (int ch = 0; ch < 4; ++ch) {
-        if (!isChecked(c, ch)) {
-          updateFlag(c, ch);
-          if (!siIsEmpty(S(c), ch)) {
-            int ns = nextState(c, ch);
+        if (!(C.state & (1 << ch))) {
+          C.state |= 1 << ch;
+          storeStateWord(c, C.state);
+          if (!siIsEmpty(C, ch)) {
+            const int ns = nextStateLocal(c, C, ch);
             if (ns == -2) return;
             if (ns >= 0) queueAdd(update(base, c, ns));
           }
         }
       }
-      updateSplitFlag(c);
+      C.state |= 1 << 4;  // updateSplitFlag
+      storeStateWord(c, C.state);
       if (numSplit(base) < cfg.numSplit && nm + 1 <= minMismatches) {
-        const int index = cNextIdx(S(c));
+        const int index = cNextIdx(C);
         if (index > cfg.indelEndSkip && m - index >= cfg.indelEndSkip) {
           int ns = nextStateAfterSplit(c, false);
           if (ns == -2) return;
@@ -1135,6 +1298,67 @@ struct BsfLane {
     }
   }
 
+  // ---- register cache of the most recently created state (the usual next poll) ----
+  int cacheIdx = -1;
+  DState<R> cache;
+  GWA_HD void loadState(int idx, DState<R> &d) {
+    if (idx == cacheIdx) d = cache;
+    else d = L.arena[idx];
+  }
+  GWA_HD void storeStateWord(int idx, int32_t w) {
+    L.arena[idx].state = w;
+    if (idx == cacheIdx) cache.state = w;
+  }
+  GWA_HD void invalidateCache() { cacheIdx = -1; }
+  GWA_HD int qcode(int strand, int i) const { return (int)((qword(strand, i >> 5) >> (2 * (i & 31))) & 3); }
+  // one chain member's term of score()/upperBoundOfScore() with ns splits after it
+  GWA_HD int stateScore(const DState<R> &d, int ns, bool upper) const {
+    const int nm = (int)(((uint32_t)d.state >> 8) & 0xFF) - ns;
+    const int mm = cProcessed(d) + (upper ? cRemaining(d) : 0) - nm;
+    return mm * cfg.matchScore - nm * cfg.mismatchPenalty - ns * cfg.splitOpenPenalty;
+  }
+  // SearchState.nextState (:840-852) from a register copy of the parent; the child stays cached
+  GWA_HD int nextStateLocal(int c, const DState<R> &cs, int ch) {
+    const int strand = cStrand(cs);
+    uint64_t rows[R];
+    int nh = 0, nko = 0;
+    bool hm = false;
+    DState<R> d;
+    d.meta = 0;
+    nextSi(cs, ch, d);  // the FM step (next(c, ch)) precedes the automaton (:422-425)
+    ++numFMIndexSearches;
+    tr(2, (uint32_t)ch, d.lb[0] ^ (d.ub[1] * 3u) ^ (d.lb[2] * 7u) ^ (d.ub[3] * 11u) ^ d.bBase, (uint32_t)(d.meta & 3));
+    if (!nfaNext(cs, ch, strand, rows, &nh, &nko, &hm)) { tr(3, 0, 0, 0); return -1; }
+    tr(4, (uint32_t)nh | ((uint32_t)nko << 8) | ((uint32_t)hm << 16), (uint32_t)rows[0], (uint32_t)(nh > 1 ? rows[1] : 0));
+    int id = allocState();
+    if (id < 0) return -2;
+    int nc = cs.cursor, dir = cDir(cs);
+    if (dir == D_FORWARD) ++nc;
+    else if (dir == D_BACKWARD) --nc;
+    else {
+      if (nc + 1 < cs.end) ++nc;
+      else { dir = D_BACKWARD; nc = cs.pivot; }
+    }
+    setCursor(d, strand, dir, cs.start, cs.end, nc, cs.pivot);
+    uint32_t sl = 0, su = 0;
+    bool sv = dir != D_BACKWARD ? siGetF(cs, ch, &sl, &su) : siGetB(cs, ch, &sl, &su);
+    d.curLb = sv ? sl : 0;
+    d.curUb = sv ? su : 0;
+    if (sv) d.meta |= M_CURVALID;
+    d.meta |= M_NFAVALID;
+    d.state = packState(ch, nko, (int)(((uint32_t)cs.state >> 16) & 0xFF), hm);
+    d.nextSplit = cs.nextSplit;
+    d.nrows = (uint8_t)nh;
+    d.kOffset = (uint8_t)nko;
+#pragma unroll
+    for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
+    L.arena[id] = d;
+    cache = d;
+    cacheIdx = id;
+    (void)c;
+    return id;
+  }
+
   // AlignmentProcess.align (:210-268) minus the record conversion (host side, sam.cpp)
   GWA_HD void initRead(const uint8_t *codes, int m_) {
     rd = codes;
@@ -1145,6 +1369,7 @@ struct BsfLane {
     bestScore = -1;
     numFMIndexSearches = 0;
     nStates = heapSize = nHits = listSize = nCigar = 0;
+    cacheIdx = -1;
     status = ST_UNMAPPED;
     quickSteps = blocks = saReads = 0;
   }

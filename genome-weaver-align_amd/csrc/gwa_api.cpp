@@ -418,7 +418,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       const int bMax = std::max(1, (m + 63) / 64);
       const int nref = m + 2 * b->kmax + 2;
       caps.dpWords = 2 * bMax * (nref + 1);
-      caps.path = ((m + nref + 8) + 7) & ~7;
+      caps.path = ((m + 2 * nref + 16) + 7) & ~7;
       const uint64_t stride = laneBytesFor(b->R, caps);
       uint32_t lanes = std::min<uint32_t>(n, T.maxLanes);
       lanes = (lanes + 255) / 256 * 256;

@@ -25,7 +25,7 @@ static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int max
                   const char *const *names, const char *const *seqs, const char *const *quals, std::string &sam,
                   int32_t *stats) {
   const int bMax = std::max(1, (maxM + 63) / 64), nref = maxM + 2 * kmax + 2;
-  const int dpw = 2 * bMax * (nref + 1), path = ((maxM + nref + 8) + 7) & ~7;
+  const int dpw = 2 * bMax * (nref + 1), path = ((maxM + 2 * nref + 16) + 7) & ~7;
   const Caps tiers[3] = {{256, 256, 32, 32, 512, dpw, path}, {4096, 4096, 256, 256, 4096, dpw, path},
                          {65536, 65536, 4096, 4096, 65536, dpw, path}};
   std::vector<uint8_t> scratch(laneBytes<R>(tiers[2]) + 4096);
