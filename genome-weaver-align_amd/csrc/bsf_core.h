@@ -30,6 +30,28 @@ GWA_HD T pinv(T x) {
 #endif
   return x;
 }
+// Region timers of the search loop (profiling builds only, -DGWA_PROF): the delta of the
+// shader clock across a region is charged once per wavefront (first active lane), so summing over
+// lanes gives wavefront cycles spent per region.
+#if defined(GWA_PROF) && defined(__HIP_DEVICE_COMPILE__)
+#define GWA_PT(v) const uint64_t v = clock64()
+#define GWA_PA(r, v)                                                            \
+  do {                                                                          \
+    const uint64_t d_ = clock64() - (v);                                        \
+    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) prof[r] += d_;      \
+  } while (0)
+// GWA_PC(w, l): count one wavefront execution in slot w and one lane execution in slot l
+#define GWA_PC(w, l)                                                            \
+  do {                                                                          \
+    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) prof[w] += 1;       \
+    prof[l] += 1;                                                               \
+  } while (0)
+#else
+#define GWA_PT(v)
+#define GWA_PA(r, v)
+#define GWA_PC(w, l)
+#endif
+
 template <class T, int N>
 GWA_HD T pick(const T (&a)[N], int i) {
   T v = pinv(a[0]);
@@ -130,56 +152,108 @@ struct DHit {
 
 // per-lane scratch capacities (entries)
 struct Caps {
-  int32_t arena, heap, hits, list, cigar, dpWords, path;
+  int32_t arena, heap, hits, list, cigar, dpWords, path, wr;
 };
 
+// Per-lane scratch.  The search structures (arena/heap/hits/list/cigar) sit in a per-lane slice;
+// the DP history, the per-column DP flags and the traceback path are "interleaved": element e of
+// this lane lives at ptr[e * is].  On the GPU is = 64 and a wavefront's 64 lanes are adjacent, so
+// the lock-step DP column stores of a wavefront coalesce into one contiguous line per store.
 template <int R>
 struct LaneMem {
-  DState<R> *arena;
-  uint64_t *heap;  // PriorityQueue array of (key << 16 | state index); key cached, refreshed on mutation
-  DHit *hits;
-  int32_t *list;
-  uint16_t *cigar;
-  uint64_t *dp;
-  uint8_t *path;
-  uint64_t *masks;  // [strand 2][F/R 2][ch 4][block 4]
+  // two base pointers + uniform offsets (kept in SGPRs), not eight per-lane pointers
+  uint8_t *slice;          // this lane's slice: arena | heap | hits | list | cigar
+  uint8_t *chunk;          // interleaved block (the wavefront's on the GPU, the lane's on the host)
+  uint32_t oHeap, oHits, oList, oCigar;  // byte offsets in the slice
+  uint32_t oWr, oPath;     // byte offsets of the wr / path planes in the chunk
+  int lane, is;            // lane in the interleaved block, interleave stride (elements)
+  GWA_HD DState<R> *arena() const { return (DState<R> *)slice; }
+  GWA_HD uint64_t *heap() const { return (uint64_t *)(slice + oHeap); }  // PriorityQueue array of (key << 16 | state index)
+  GWA_HD DHit *hits() const { return (DHit *)(slice + oHits); }
+  GWA_HD int32_t *list() const { return (int32_t *)(slice + oList); }
+  GWA_HD uint16_t *cigar() const { return (uint16_t *)(slice + oCigar); }
+  GWA_HD uint64_t *dp() const { return (uint64_t *)chunk + lane; }   // [2][col 0..N][block] vp / vn history
+  GWA_HD uint8_t *wr() const { return chunk + oWr + lane; }          // [col 0..N] blocks computed (bits 0-3) / activated (4-7)
+  GWA_HD uint8_t *path() const { return chunk + oPath + lane; }      // traceback path
 };
 
 template <int R>
-GWA_HD size_t laneBytes(const Caps &c) {
+GWA_HD size_t laneBytes(const Caps &c) {  // per-lane slice
   size_t b = 0;
   b += sizeof(DState<R>) * (size_t)c.arena;
   b += 8 * (size_t)c.heap;
   b += sizeof(DHit) * (size_t)c.hits;
   b += 4 * (size_t)c.list;
   b += 2 * (size_t)c.cigar;
-  b = (b + 7) & ~(size_t)7;
-  b += 8 * (size_t)c.dpWords;
-  b += 8 * 64;
-  b += (size_t)c.path;
   return (b + 255) & ~(size_t)255;
 }
+GWA_HD size_t ilvBytes(const Caps &c) {  // interleaved bytes per lane
+  return (8 * (size_t)c.dpWords + (size_t)c.wr + (size_t)c.path + 7) & ~(size_t)7;
+}
 
+// slice = this lane's slice; chunk = its wavefront's interleaved block (64 lanes, is = 64), or the
+// lane's own interleaved block (is = 1, host builds)
 template <int R>
-GWA_HD LaneMem<R> laneMem(uint8_t *base, const Caps &c) {
+GWA_HD LaneMem<R> laneMem(uint8_t *slice, uint8_t *chunk, int laneInWave, int is, const Caps &c) {
   LaneMem<R> L;
-  size_t b = 0;
-  L.arena = (DState<R> *)(base + b); b += sizeof(DState<R>) * (size_t)c.arena;
-  L.heap = (uint64_t *)(base + b); b += 8 * (size_t)c.heap;
-  L.hits = (DHit *)(base + b); b += sizeof(DHit) * (size_t)c.hits;
-  L.list = (int32_t *)(base + b); b += 4 * (size_t)c.list;
-  L.cigar = (uint16_t *)(base + b); b += 2 * (size_t)c.cigar;
-  b = (b + 7) & ~(size_t)7;
-  L.dp = (uint64_t *)(base + b); b += 8 * (size_t)c.dpWords;
-  L.masks = (uint64_t *)(base + b); b += 8 * 64;
-  L.path = base + b;
+  size_t b = sizeof(DState<R>) * (size_t)c.arena;
+  L.slice = slice;
+  L.oHeap = (uint32_t)b; b += 8 * (size_t)c.heap;
+  L.oHits = (uint32_t)b; b += sizeof(DHit) * (size_t)c.hits;
+  L.oList = (uint32_t)b; b += 4 * (size_t)c.list;
+  L.oCigar = (uint32_t)b;
+  L.chunk = chunk;
+  L.oWr = (uint32_t)((size_t)is * 8 * c.dpWords);
+  L.oPath = (uint32_t)((size_t)is * (8 * (size_t)c.dpWords + (size_t)c.wr));
+  L.lane = laneInWave;
+  L.is = is;
   return L;
 }
+template <int R>
+GWA_HD LaneMem<R> laneMem(uint8_t *base, const Caps &c) {  // host: one lane, is = 1
+  return laneMem<R>(base, base + laneBytes<R>(c), 0, 1, c);
+}
+
+// Streaming reader of reference codes (0-3, 4 = N) over the 2-bit text + N bitmap.  The word after
+// (fwd) or before (back) the current one is loaded one word ahead, so a column walk waits on HBM
+// once per 32 columns at most instead of once per column.
+struct RefCursor {
+  const uint64_t *t2, *tn;
+  int64_t last2, lastN;                 // last valid word indices
+  int64_t a2 = -4, an = -4;             // word indices held in c2 / cn
+  uint64_t c2 = 0, cn = 0, x2 = 0, xn = 0;  // current words, prefetched neighbours
+  int64_t xa2 = -4, xan = -4;           // indices of the prefetched neighbours
+  GWA_HD RefCursor(const uint64_t *t2_, const uint64_t *tn_, uint64_t N)
+      : t2(t2_), tn(tn_), last2(N ? (int64_t)((N - 1) >> 5) : 0), lastN(N ? (int64_t)((N - 1) >> 6) : 0) {}
+  GWA_HD int code(int64_t p, int dir) {
+    const int64_t a = p >> 5, b = p >> 6;
+    if (a != a2) {
+      c2 = a == xa2 ? x2 : t2[a];
+      a2 = a;
+      int64_t na = a + dir;
+      na = na < 0 ? 0 : na > last2 ? last2 : na;
+      xa2 = na;
+      x2 = t2[na];
+    }
+    if (b != an) {
+      cn = b == xan ? xn : tn[b];
+      an = b;
+      int64_t nb = b + dir;
+      nb = nb < 0 ? 0 : nb > lastN ? lastN : nb;
+      xan = nb;
+      xn = tn[nb];
+    }
+    return ((cn >> (p & 63)) & 1) ? 4 : (int)((c2 >> ((p & 31) * 2)) & 3);
+  }
+};
 
 struct Overflow {};  // thrown only on host test builds; device uses status codes
 
-template <int R>
+// QW = 2-bit query words per strand held in registers (4: reads <= 128 bp, 8: <= 255 bp); the
+// DP then needs at most DB = QW / 2 blocks of 64 rows.
+template <int R, int QW = 8>
 struct BsfLane {
+  static constexpr int DB = QW / 2;
   const IndexView &ix;
   const SearchConfig &cfg;
   const StairTables &st;
@@ -199,6 +273,9 @@ struct BsfLane {
   // debug trace (nullptr in production launches): 4 words per event
   uint32_t *trace = nullptr;
   int traceCap = 0, traceN = 0;
+#ifdef GWA_PROF
+  uint64_t prof[PR_N] = {};
+#endif
   GWA_HD void tr(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     if (!trace || traceN + 4 > traceCap) return;
     trace[traceN++] = a; trace[traceN++] = b; trace[traceN++] = c; trace[traceN++] = d;
@@ -230,15 +307,14 @@ struct BsfLane {
   GWA_HD void rank2(int fm, uint64_t lb, uint64_t ub, uint64_t lo[5], uint64_t hi[5]) {
     if (lb > ix.N) lb = ix.N;
     if (ub > ix.N) ub = ix.N;
-    Block B;
-    loadBlock(ix.occ[fm], lb >> 7, B);
-    ++blocks;
-    rankAll(B, lb, lo);
-    if ((ub >> 7) != (lb >> 7)) {
-      loadBlock(ix.occ[fm], ub >> 7, B);
-      ++blocks;
-    }
-    rankAll(B, ub, hi);
+    // both blocks are requested before either is used: one memory round trip, not two
+    const int two = (ub >> 7) != (lb >> 7);
+    Block B0, B1;
+    loadBlock(ix.occ[fm], lb >> 7, B0);
+    loadBlock(ix.occ[fm], ub >> 7, B1);  // same line when !two (an L2 hit)
+    blocks += 1 + two;
+    rankAll(B0, lb, lo);
+    rankAll(B1, ub, hi);
   }
 
   // ---- SequenceBoundary.translate (A/SequenceBoundary.java:104-121): last offset < textIndex ----
@@ -259,19 +335,19 @@ struct BsfLane {
   // The read (after replaceN_withA) is kept 2-bit packed in registers for both strands:
   // qw[s][w] holds positions 32w..32w+31.  A 64-bit pattern window is a funnel shift of three
   // words, a 2-bit compare and an even-bit compress (no per-read mask arrays in memory).
-  uint64_t qw[2][8];
+  uint64_t qw[2][QW];
   GWA_HD void buildMasks() {
-    for (int s2 = 0; s2 < 2; ++s2)
-      for (int w = 0; w < 8; ++w) qw[s2][w] = 0;
+    // (the inner loop stays rolled: fully unrolled, its byte loads would all be in flight at once)
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
+    for (int w = 0; w < QW; ++w) {
       uint64_t v0 = 0, v1 = 0;
-      for (int j = 0; j < 32; ++j) {
-        const int i = w * 32 + j;
-        if (i < m) {
-          v0 |= (uint64_t)q(0, i) << (2 * j);
-          v1 |= (uint64_t)q(1, i) << (2 * j);
-        }
+      const int n = m - w * 32 < 32 ? m - w * 32 : 32;
+#pragma unroll 1
+      for (int j = 0; j < n; ++j) {
+        const int c = rd[w * 32 + j];
+        const uint64_t c0 = c >= 4 ? 0 : c, c1 = c >= 4 ? 0 : 3 - c;  // q(0, i), q(1, i)
+        v0 |= c0 << (2 * j);
+        v1 |= c1 << (2 * j);
       }
       qw[0][w] = v0;
       qw[1][w] = v1;
@@ -280,7 +356,9 @@ struct BsfLane {
   GWA_HD uint64_t qword(int strand, int w) const {
     uint64_t v = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v = (w == i) ? (strand ? qw[1][i] : qw[0][i]) : v;
+    for (int i = 0; i < QW; ++i) v = (strand * QW + w == i) ? qw[0][i] : v;
+#pragma unroll
+    for (int i = 0; i < QW; ++i) v = (strand * QW + w == QW + i) ? qw[1][i] : v;
     return v;
   }
   GWA_HD static uint64_t compressEven(uint64_t x) {
@@ -339,13 +417,16 @@ struct BsfLane {
     return p;
   }
   // StaircaseFilter.getStairCaseMask64bit via the host-built table (S/StaircaseFilter.java:91-102)
+  // this read's table (resolved once per read in initRead; LDS when the kernel staged it)
+  const uint64_t *stairLds = nullptr;
+  const uint64_t *stairTab = nullptr;
+  int stairBad = 0;
   GWA_HD int64_t stairMask(int row, int offset) {
     const int kk = minMismatches;
     if (row >= kk + 1) return 0;
     const int km = st.kmax;
-    uint32_t base = st.base[m];
-    if (base >= 0xFFFFFFFEu) { status = ST_ERROR; return 0; }  // StaircaseFilter ctor throws for this m
-    return (int64_t)st.tab[base + ((size_t)(kk * (km + 1) + row) * (size_t)(m + km + 1) + (size_t)(offset + km))];
+    if (stairBad) { status = ST_ERROR; return 0; }  // StaircaseFilter ctor throws for this m
+    return (int64_t)stairTab[(size_t)(kk * (km + 1) + row) * (size_t)(m + km + 1) + (size_t)(offset + km)];
   }
 
   // ---- Cursor (S/Cursor.java) ----
@@ -411,7 +492,7 @@ struct BsfLane {
   }
 
   // ---- state flags ----
-  GWA_HD DState<R> &S(int i) { return L.arena[i]; }
+  GWA_HD DState<R> &S(int i) { return L.arena()[i]; }
   GWA_HD int minK(int s) { return (int)(((uint32_t)S(s).state >> 8) & 0xFF); }
   GWA_HD void setMinK(int s, int d) {
     invalidateCache();
@@ -488,51 +569,148 @@ struct BsfLane {
   }
   GWA_HD void refreshKeys() {
     for (int i = 0; i < heapSize; ++i) {
-      const int idx = (int)(L.heap[i] & 0xFFFF);
-      L.heap[i] = (keyOf(idx) << 16) | (uint64_t)idx;
+      const int idx = (int)(L.heap()[i] & 0xFFFF);
+      L.heap()[i] = (keyOf(idx) << 16) | (uint64_t)idx;
     }
   }
-  // java.util.PriorityQueue.offer / poll on cached keys
+  // java.util.PriorityQueue.offer / poll on cached keys.  The element moves are exactly Java's
+  // siftUp / siftDown; only the loads are reordered: offer reads the whole ancestor path (up to
+  // 8 levels) at once, poll reads children and grandchildren together, so a heap operation waits
+  // on memory once per 8 (offer) or 2 (poll) levels instead of once per level.
+#ifdef GWA_SIMPLE_ADD
   GWA_HD void queueAddKeyed(uint64_t e) {
     if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
     int kk = heapSize++;
     const uint64_t ek = e >> 16;
     while (kk > 0) {
       int parent = (kk - 1) >> 1;
-      uint64_t p = L.heap[parent];
+      uint64_t p = L.heap()[parent];
       if (ek >= (p >> 16)) break;
-      L.heap[kk] = p;
+      L.heap()[kk] = p;
       kk = parent;
     }
-    L.heap[kk] = e;
+    L.heap()[kk] = e;
   }
-  GWA_HD void queueAdd(int e) {
-    if (e < 0) return;
-    queueAddKeyed((keyOf(e) << 16) | (uint64_t)e);
+#else
+  GWA_HD void queueAddKeyed(uint64_t e) {
+    if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
+    const int kk = heapSize++;
+    const uint64_t ek = e >> 16;
+    constexpr int MAXD = 8;
+    uint64_t av[MAXD];
+    int ai[MAXD];
+    {
+      int idx = kk;
+#pragma unroll
+      for (int d = 0; d < MAXD; ++d) {
+        const int p = idx > 0 ? (idx - 1) >> 1 : 0;
+        ai[d] = p;
+        av[d] = L.heap()[p];
+        idx = p;
+      }
+    }
+    // Java's siftUp stops at the first ancestor d with ek >= key (the cached keys need not be
+    // heap-ordered after a refresh, so this is a first-match, not a count).  Selects only: no
+    // loop-carried flag (see quickScan).
+    const int depth = 31 - __builtin_clz((unsigned)kk + 1u);
+    int t = MAXD;
+#pragma unroll
+    for (int d = MAXD - 1; d >= 0; --d) t = (d >= depth || ek >= (av[d] >> 16)) ? d : t;
+#pragma unroll
+    for (int d = 0; d < MAXD; ++d)
+      if (d < t) L.heap()[d == 0 ? kk : ai[d - 1]] = av[d];
+    int pos = t == 0 ? kk : pick(ai, t - 1);
+    if (t == MAXD) {  // deeper than MAXD levels (large tiers only): Java's loop from there
+      while (pos > 0) {
+        const int parent = (pos - 1) >> 1;
+        const uint64_t p = L.heap()[parent];
+        if (ek >= (p >> 16)) break;
+        L.heap()[pos] = p;
+        pos = parent;
+      }
+    }
+    L.heap()[pos] = e;
+    tr(9, (uint32_t)(e & 0xFFFF), (uint32_t)kk, (uint32_t)pos);
   }
+#endif
+#ifdef GWA_SIMPLE_POLL
   GWA_HD int queuePoll() {
     if (heapSize == 0) return -1;
     int s = --heapSize;
-    const uint64_t result = L.heap[0];
-    const uint64_t x = L.heap[s];
+    const uint64_t result = L.heap()[0];
+    const uint64_t x = L.heap()[s];
     if (s != 0) {
       int kk = 0, half = heapSize >> 1;
       const uint64_t xk = x >> 16;
       while (kk < half) {
         int child = (kk << 1) + 1;
-        uint64_t c = L.heap[child];
+        uint64_t c = L.heap()[child];
         int right = child + 1;
         if (right < heapSize) {
-          uint64_t rc = L.heap[right];
+          uint64_t rc = L.heap()[right];
           if ((c >> 16) > (rc >> 16)) { c = rc; child = right; }
         }
         if (xk <= (c >> 16)) break;
-        L.heap[kk] = c;
+        L.heap()[kk] = c;
         kk = child;
       }
-      L.heap[kk] = x;
+      L.heap()[kk] = x;
     }
     return (int)(result & 0xFFFF);
+  }
+#else
+  GWA_HD int queuePoll() {
+    if (heapSize == 0) return -1;
+    int s = --heapSize;
+    const uint64_t result = L.heap()[0];
+    const uint64_t x = L.heap()[s];
+    if (s != 0) {
+      const int n = heapSize, half = n >> 1, capm1 = caps.heap - 1;
+      int kk = 0;
+      const uint64_t xk = x >> 16;
+      int go = kk < half;  // single-exit loop (no break): see quickScan
+      while (go) {
+        // children c0,c1 and grandchildren g0..g3 of kk (indices clamped into the array; entries
+        // at or past n are never selected)
+        const int c = (kk << 1) + 1;
+        const int g = (kk << 2) + 3;
+        const uint64_t c0 = L.heap()[c], c1 = L.heap()[c + 1 <= capm1 ? c + 1 : capm1];
+        const uint64_t g0 = L.heap()[g <= capm1 ? g : capm1], g1 = L.heap()[g + 1 <= capm1 ? g + 1 : capm1];
+        const uint64_t g2 = L.heap()[g + 2 <= capm1 ? g + 2 : capm1], g3 = L.heap()[g + 3 <= capm1 ? g + 3 : capm1];
+        // level 1
+        const int right = (c + 1 < n && (c0 >> 16) > (c1 >> 16)) ? 1 : 0;
+        const uint64_t cv = right ? c1 : c0;
+        if (xk <= (cv >> 16)) {
+          go = 0;
+        } else {
+          L.heap()[kk] = cv;
+          kk = c + right;
+          go = kk < half;
+        }
+        // level 2: the children of c are g0,g1, those of c+1 are g2,g3
+        if (go) {
+          const int c2 = (kk << 1) + 1;
+          const uint64_t d0 = right ? g2 : g0, d1 = right ? g3 : g1;
+          const int right2 = (c2 + 1 < n && (d0 >> 16) > (d1 >> 16)) ? 1 : 0;
+          const uint64_t dv = right2 ? d1 : d0;
+          if (xk <= (dv >> 16)) {
+            go = 0;
+          } else {
+            L.heap()[kk] = dv;
+            kk = c2 + right2;
+            go = kk < half;
+          }
+        }
+      }
+      L.heap()[kk] = x;
+    }
+    tr(10, (uint32_t)(result & 0xFFFF), (uint32_t)heapSize, (uint32_t)(x & 0xFFFF));
+    return (int)(result & 0xFFFF);
+  }
+#endif
+  GWA_HD void queueAdd(int e) {
+    if (e < 0) return;
+    queueAddKeyed((keyOf(e) << 16) | (uint64_t)e);
   }
 
   // ---- FMQuickScan.scanMismatchLocations (S/FMQuickScan.java:66-94) ----
@@ -585,30 +763,30 @@ struct BsfLane {
   // ---- hits (R/ReadHit.java) ----
   GWA_HD int newHit(int32_t chr, int32_t pos, int ml, int qs, int qe, int diff, int strand, int cigOff, int cigLen, int numHits) {
     if (nHits >= caps.hits) { status = ST_OVERFLOW; return -1; }
-    DHit &h = L.hits[nHits];
+    DHit &h = L.hits()[nHits];
     h.chr = chr; h.pos = pos; h.matchLength = ml; h.qStart = qs; h.qEnd = qe; h.diff = diff; h.strand = strand;
     h.numHits = numHits; h.next = -1; h.cigarOff = cigOff; h.cigarLen = cigLen; h.pad = 0;
     return nHits++;
   }
   GWA_HD int putCigarOp(int type, int len) {
     if (nCigar >= caps.cigar) { status = ST_OVERFLOW; return -1; }
-    L.cigar[nCigar++] = (uint16_t)((len << 3) | type);
+    L.cigar()[nCigar++] = (uint16_t)((len << 3) | type);
     return 0;
   }
   GWA_HD int hitTotalDiff(int h) {
     int d = 0;
-    for (int t = h; t >= 0; t = L.hits[t].next) d += L.hits[t].diff + (L.hits[t].next >= 0 ? 1 : 0);
+    for (int t = h; t >= 0; t = L.hits()[t].next) d += L.hits()[t].diff + (L.hits()[t].next >= 0 ? 1 : 0);
     return d;
   }
   GWA_HD int hitTotalMatch(int h) {
     int d = 0;
-    for (int t = h; t >= 0; t = L.hits[t].next) d += L.hits[t].matchLength;
+    for (int t = h; t >= 0; t = L.hits()[t].next) d += L.hits()[t].matchLength;
     return d;
   }
   GWA_HD int hitTotalScore(int h) {
     int sc = 0;
-    for (int t = h; t >= 0; t = L.hits[t].next) {
-      const DHit &x = L.hits[t];
+    for (int t = h; t >= 0; t = L.hits()[t].next) {
+      const DHit &x = L.hits()[t];
       sc += x.matchLength * cfg.matchScore - x.diff * cfg.mismatchPenalty;
       if (x.next >= 0) sc -= cfg.splitOpenPenalty;
     }
@@ -626,24 +804,24 @@ struct BsfLane {
     if (maxMatchLength < matchLen) maxMatchLength = matchLen;
     int n = 0;
     for (int i = 0; i < listSize; ++i) {
-      int e = L.list[i];
-      if (hitTotalDiff(e) <= minMismatches && hitTotalMatch(e) >= maxMatchLength) L.list[n++] = e;
+      int e = L.list()[i];
+      if (hitTotalDiff(e) <= minMismatches && hitTotalMatch(e) >= maxMatchLength) L.list()[n++] = e;
     }
     if (n >= caps.list) { status = ST_OVERFLOW; listSize = n; return; }
-    L.list[n++] = hit;
+    L.list()[n++] = hit;
     listSize = n;
   }
 
   // ReadHit.sortSplits (R/ReadHit.java:148-182): stable insertion sort of the chain
   GWA_HD int sortSplits(int head) {
-    if (L.hits[head].next < 0) return head;
+    if (L.hits()[head].next < 0) return head;
     int arr[8];
     int n = 0;
-    for (int t = head; t >= 0; t = L.hits[t].next) {
+    for (int t = head; t >= 0; t = L.hits()[t].next) {
       if (n >= 8) { status = ST_OVERFLOW; return head; }
       arr[n++] = t;
     }
-    const int headStrand = L.hits[head].strand;
+    const int headStrand = L.hits()[head].strand;
     for (int i = 1; i < n; ++i) {
       int x = arr[i];
       int j = i - 1;
@@ -656,13 +834,13 @@ struct BsfLane {
       }
       arr[j + 1] = x;
     }
-    for (int i = 0; i + 1 < n; ++i) L.hits[arr[i]].next = arr[i + 1];
-    L.hits[arr[n - 1]].next = -1;
+    for (int i = 0; i + 1 < n; ++i) L.hits()[arr[i]].next = arr[i + 1];
+    L.hits()[arr[n - 1]].next = -1;
     return arr[0];
   }
   GWA_HD int cmpHit(int a, int b, int headStrand) {
-    const DHit &o1 = L.hits[a];
-    const DHit &o2 = L.hits[b];
+    const DHit &o1 = L.hits()[a];
+    const DHit &o2 = L.hits()[b];
     int diff = 0;
     if (o1.chr == CHR_NULL || o2.chr == CHR_NULL) {
       diff = o1.qStart - o2.qStart;
@@ -718,14 +896,14 @@ struct BsfLane {
     const int kb = cfg.bandWidth;
     const int bMax = mq + w - 1 >= w ? (mq + w - 1) / w : 1;
     const int N = (int)(refEnd - refStart);
-    if (bMax > 4 || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || mq + 2 * N + 4 > caps.path) { status = ST_OVERFLOW; return -1; }
-    uint64_t pA[4] = {0, 0, 0, 0}, pC[4] = {0, 0, 0, 0}, pG[4] = {0, 0, 0, 0}, pT[4] = {0, 0, 0, 0};
+    if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || mq + N + 2 > caps.path || N + 1 > caps.wr) { status = ST_OVERFLOW; return -1; }
+    uint64_t pA[DB] = {}, pC[DB] = {}, pG[DB] = {}, pT[DB] = {};
     for (int p = 0; p < mq; ++p) {
       const int c = dpQ(strand, qs, qe, p);
       const uint64_t bit = 1ULL << (p & 63);
       const int b = p >> 6;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < DB; ++r) {
         if (r == b) {
           if (c == 0) pA[r] |= bit;
           else if (c == 1) pC[r] |= bit;
@@ -734,104 +912,111 @@ struct BsfLane {
         }
       }
     }
-    uint64_t *hvp = L.dp;                         // [col 1..N][block] history
-    uint64_t *hvn = L.dp + (size_t)bMax * (N + 1);
-    uint8_t *wr = L.path + mq + N + 2;            // per column: bits 0-3 computed, bits 4-7 activated-as-input
-    for (int j = 0; j <= N; ++j) wr[j] = 0;
-    uint64_t vp[4], vn[4];
-    int D[4] = {0, 0, 0, 0}, sb[4];
+    const size_t is = (size_t)L.is;
+    uint64_t *hvp = L.dp();                          // [col 1..N][block] history
+    uint64_t *hvn = L.dp() + is * bMax * (N + 1);
+    uint8_t *wr = L.wr();                            // per column: bits 0-3 computed, bits 4-7 activated-as-input
+    uint64_t vp[DB], vn[DB];
+    int D[DB] = {}, sb[DB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < DB; ++r) {
       vp[r] = ~0ULL;
       vn[r] = 0;
       const int v = mq - ((r + 1) * w) + kb;
       sb[r] = v > 0 ? v : 0;
     }
-    wr[0] = (uint8_t)(((1 << bMax) - 1) << 4);  // column 0 inputs: ~0 / 0 for every block
+    uint32_t pend = (uint32_t)(((1 << bMax) - 1) << 4);  // column 0 inputs: ~0 / 0 for every block
     D[0] = mq;
     int bCeil = (kb + w - 1) / w;
     if (bCeil < 1) bCeil = 1;
     int have = 0;  // int, not bool: see quickScan
     int bestTail = 0, bestDiff = 0;
+    RefCursor rc(ix.text2, ix.textN, ix.N);
     for (int j = 0; j < N; ++j) {
-      const int ch = refCode(refStart + j);
+      const int ch = rc.code(refStart + j, 1);
       int carry = 0;
-      uint8_t wmask = 0;
+      uint32_t wmask = 0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < DB; ++r) {
         if (r < bCeil) {
           const uint64_t x = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
           const int ns = dpBlock(x, carry, vp[r], vn[r]);
           D[r] += ns;
           carry = ns;
-          hvp[(size_t)(j + 1) * bMax + r] = vp[r];
-          hvn[(size_t)(j + 1) * bMax + r] = vn[r];
-          wmask |= (uint8_t)(1 << r);
+          hvp[((size_t)(j + 1) * bMax + r) * is] = vp[r];
+          hvn[((size_t)(j + 1) * bMax + r) * is] = vn[r];
+          wmask |= 1u << r;
         }
       }
       const int dPrev = pick(D, bCeil - 1);
       const uint64_t nextPeq = ch == 0 ? pick(pA, bCeil) : ch == 1 ? pick(pC, bCeil) : ch == 2 ? pick(pG, bCeil) : ch == 3 ? pick(pT, bCeil) : 0ULL;
       if (bCeil < bMax && dPrev - carry <= pick(sb, bCeil - 1) && (((nextPeq & 1ULL) != 0ULL) || carry < 0)) {
         // activate block bCeil with input column j = ~0 / 0 (:427-428)
-        wr[j] |= (uint8_t)(1 << (4 + bCeil));
+        pend |= 1u << (4 + bCeil);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < DB; ++r) {
           if (r == bCeil) {
             vp[r] = ~0ULL;
             vn[r] = 0ULL;
             const uint64_t x = nextPeq;
             const int ns = dpBlock(x, carry, vp[r], vn[r]);
             D[r] = dPrev - carry + ns;
-            hvp[(size_t)(j + 1) * bMax + r] = vp[r];
-            hvn[(size_t)(j + 1) * bMax + r] = vn[r];
-            wmask |= (uint8_t)(1 << r);
+            hvp[((size_t)(j + 1) * bMax + r) * is] = vp[r];
+            hvn[((size_t)(j + 1) * bMax + r) * is] = vn[r];
+            wmask |= 1u << r;
           }
         }
         bCeil++;
       } else {
         while (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
       }
-      wr[j + 1] |= wmask;
+      wr[(size_t)j * is] = (uint8_t)pend;
+      pend = wmask;
       if (bCeil == bMax) {
         const int dl = pick(D, bCeil - 1);
         if (!have) { have = 1; bestTail = j; bestDiff = dl; continue; }
         if (bestDiff > dl) { bestTail = j; bestDiff = dl; }
       }
     }
+    wr[(size_t)N * is] = (uint8_t)pend;
     (void)bestDiff;
     if (!have) return 1;
-    // traceback (:515-643); path chars are appended in reverse order into L.path
-    uint8_t *path = L.path;
+    // traceback (:515-643); path chars are appended in reverse order into L.path().  A match decides
+    // the step from the codes alone (:547), so the history is read only at edits.
+    uint8_t *path = L.path();
     int plen = 0;
     int row = mq - 1, col = bestTail;
     int diff = 0, leftMostPos = 0;
     for (;;) {
       int pth = 0;  // 0 NONE 1 DIAG 2 DIAG_MM 3 LEFT 4 UP
       if (col >= 0 && row >= 0) {
-        const int block = row >> 6, offset = row & 63;
-        const uint8_t wb = wr[col + 1];
-        uint64_t vpw = 0, vnw = 0;
-        if ((wb >> block) & 1) {  // computed at column col (the later write when both happened)
-          vpw = hvp[(size_t)(col + 1) * bMax + block];
-          vnw = hvn[(size_t)(col + 1) * bMax + block];
-          if ((wb >> (4 + block)) & 1) { vpw = ~0ULL; vnw = 0; }
-        } else if ((wb >> (4 + block)) & 1) {
-          vpw = ~0ULL;
-          vnw = 0;
+        if (rc.code(refStart + col, -1) == dpQ(strand, qs, qe, row)) {
+          pth = 1;
+        } else {
+          const int block = row >> 6, offset = row & 63;
+          const uint32_t wb = wr[(size_t)(col + 1) * is];
+          uint64_t vpw = 0, vnw = 0;
+          if ((wb >> block) & 1) {  // computed at column col (the later write when both happened)
+            vpw = hvp[((size_t)(col + 1) * bMax + block) * is];
+            vnw = hvn[((size_t)(col + 1) * bMax + block) * is];
+            if ((wb >> (4 + block)) & 1) { vpw = ~0ULL; vnw = 0; }
+          } else if ((wb >> (4 + block)) & 1) {
+            vpw = ~0ULL;
+            vnw = 0;
+          }
+          const uint64_t vpf = vpw & (1ULL << offset);
+          const uint64_t vnf = vnw & (1ULL << offset);
+          if (vpf != 0) { pth = 4; diff++; }
+          else if (vnf == 0) { pth = 2; diff++; }
+          else { pth = 3; diff++; }
         }
-        const uint64_t vpf = vpw & (1ULL << offset);
-        const uint64_t vnf = vnw & (1ULL << offset);
-        if (refCode(refStart + col) == dpQ(strand, qs, qe, row)) pth = 1;
-        else if (vpf != 0) { pth = 4; diff++; }
-        else if (vnf == 0) { pth = 2; diff++; }
-        else { pth = 3; diff++; }
       }
-      if (pth == 1 || pth == 2) { path[plen++] = 'M'; leftMostPos = col; col--; row--; }
-      else if (pth == 4) { path[plen++] = 'I'; leftMostPos = col + 1; row--; }
-      else if (pth == 3) { path[plen++] = 'D'; col--; }
+      if (pth == 1 || pth == 2) { path[plen++ * is] = 'M'; leftMostPos = col; col--; row--; }
+      else if (pth == 4) { path[plen++ * is] = 'I'; leftMostPos = col + 1; row--; }
+      else if (pth == 3) { path[plen++ * is] = 'D'; col--; }
       else {
         while (col >= 0 || row >= 0) {
-          if (row >= 0) path[plen++] = 'S';
+          if (row >= 0) path[plen++ * is] = 'S';
           col--;
           row--;
         }
@@ -841,13 +1026,13 @@ struct BsfLane {
     // cigarStr = reverse(path); leading/trailing S/I/D -> S, I/D subtract from diff
     int left = 0, right = 0;
     for (int i = 0; i < plen; ++i) {
-      const char t = (char)path[plen - 1 - i];
+      const char t = (char)path[(size_t)(plen - 1 - i) * is];
       if (t == 'S') left++;
       else if (t == 'I' || t == 'D') { left++; diff--; }
       else break;
     }
     for (int i = plen - 1; i >= left; --i) {
-      const char t = (char)path[plen - 1 - i];
+      const char t = (char)path[(size_t)(plen - 1 - i) * is];
       if (t == 'S') right++;
       else if (t == 'I' || t == 'D') { right++; diff--; }
       else break;
@@ -856,7 +1041,7 @@ struct BsfLane {
     const int off = nCigar;
     int curT = 4, curL = left;
     for (int i = left; i < plen - right; ++i) {
-      const char t = (char)path[plen - 1 - i];
+      const char t = (char)path[(size_t)(plen - 1 - i) * is];
       const int ty = t == 'M' ? 0 : t == 'I' ? 1 : t == 'D' ? 2 : 4;
       if (ty == curT) { curL++; continue; }
       if (curL > 0 && putCigarOp(curT, curL) < 0) return -1;
@@ -903,7 +1088,11 @@ struct BsfLane {
     int64_t refEnd = x + frag + k < (int64_t)ix.N ? x + frag + k : (int64_t)ix.N;
     if (refStart > refEnd) { status = ST_ERROR; return -2; }  // IllegalArgumentException in subString
     int pos = 0, diff = 0, co = 0, cl = 0;
+    GWA_PT(tv);
+    GWA_PC(PR_NVW, PR_NVL);
     int r = alignBlockDetailed(strand, d.start, d.end, refStart, refEnd, &pos, &diff, &co, &cl);
+    GWA_PA(PR_VERIFY, tv);
+    tr(7, (uint32_t)refStart, (uint32_t)(r == 0 ? pos : -1), (uint32_t)(diff | (cl << 16)));
     if (r < 0) return -2;
     if (r == 1) {
       int h = newHit(CHR_EMPTY, 0, 0, 0, 0, 0, strand, nCigar, 0, 0);
@@ -917,15 +1106,17 @@ struct BsfLane {
 
   // reportAlignment (:562-586); returns false on overflow/error
   GWA_HD bool reportAlignment(int c) {
-    int al = verify(c);
-    if (al == -2) return false;
-    for (int nx = S(c).nextSplit; nx >= 0; nx = S(nx).nextSplit) {
-      int res = verify(nx);
+    // one verify call site (the DP is large): member 0 is the chain head, the rest hang off it
+    int al = -1;
+    for (int nx = c, first = 1; nx >= 0; nx = S(nx).nextSplit, first = 0) {
+      const int res = verify(nx);
       if (res == -2) return false;
+      if (first) { al = res; continue; }
       if (al < 0) { status = ST_ERROR; return false; }
-      L.hits[al].next = res;  // nextHit is never advanced (:567-571)
+      L.hits()[al].next = res;  // nextHit is never advanced (:567-571)
     }
     if (al < 0) { status = ST_ERROR; return false; }
+    tr(8, (uint32_t)c, (uint32_t)hitTotalMatch(al), (uint32_t)hitTotalDiff(al));
     if (hitTotalMatch(al) == 0) return true;
     int newK = hitTotalDiff(al);
     if (newK > k) return true;
@@ -994,7 +1185,16 @@ struct BsfLane {
     } else {
       const int nh = height - rem;
 #pragma unroll
-      for (int h = 0; h < R; ++h) outRows[h] = h < nh ? (uint64_t)jushr(pick(next, h + rem), 1) : 0ULL;
+      for (int h = 0; h < R; ++h) outRows[h] = (uint64_t)next[h];
+      // outRows[h] = next[h + rem]: a log2(R)-stage barrel shift with static indices only
+#pragma unroll
+      for (int b = 1; b < R; b <<= 1) {
+        const int on = (rem & b) != 0;
+#pragma unroll
+        for (int h = 0; h < R; ++h) outRows[h] = on ? (h + b < R ? outRows[h + b] : 0ULL) : outRows[h];
+      }
+#pragma unroll
+      for (int h = 0; h < R; ++h) outRows[h] = h < nh ? (uint64_t)jushr((int64_t)outRows[h], 1) : 0ULL;
       *outH = nh;
     }
     *outKOff = kOff + rem;
@@ -1053,7 +1253,10 @@ struct BsfLane {
     nextSi(cs, ch, d);
     ++numFMIndexSearches;
     tr(2, (uint32_t)ch, d.lb[0] ^ (d.ub[1] * 3u) ^ (d.lb[2] * 7u) ^ (d.ub[3] * 11u) ^ d.bBase, (uint32_t)(d.meta & 3));
-    if (!nfaNext(cs, ch, strand, rows, &nh, &nko, &hm)) { tr(3, 0, 0, 0); return -1; }
+    GWA_PT(tq);
+    const bool nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm);
+    GWA_PA(PR_NFA, tq);
+    if (!nfaOk) { tr(3, 0, 0, 0); return -1; }
     tr(4, (uint32_t)nh | ((uint32_t)nko << 8) | ((uint32_t)hm << 16), (uint32_t)rows[0], (uint32_t)(nh > 1 ? rows[1] : 0));
     int id = allocState();
     if (id < 0) return -2;
@@ -1212,90 +1415,117 @@ struct BsfLane {
   }
 
   // Phase 2 (bsf_search kernel): seeds from the quick scans (:318-349) and the queue loop (:352-475)
+  // The best-first loop of searchPhase as a resumable step machine, so a wavefront can hold lanes
+  // that reached a report (the DP verification) and run those together:
+  //   searchStart: seeds (:318-341); false = nothing to search
+  //   searchStep : one loop iteration (:343-477); SS_CONTINUE, SS_REPORT (run searchReport next)
+  //                or SS_DONE
+  //   searchReport: reportAlignment of the pending chain; false = the search ended (error/overflow)
+  enum { SS_CONTINUE = 0, SS_REPORT = 1, SS_DONE = 2 };
+  int pendingBase = -1, upperSearches = 0;
   GWA_HD void searchPhase(const ScanRes &sr) {
+    if (!searchStart(sr)) return;
+    for (;;) {
+      const int st = searchStep();
+      if (st == SS_DONE) return;
+      if (st == SS_REPORT && !searchReport()) return;
+    }
+  }
+  GWA_HD bool searchReport() { return reportAlignment(pendingBase); }
+  GWA_HD bool searchStart(const ScanRes &sr) {
+    GWA_PT(tsd);
     buildMasks();
     int a = -1, b = -1;
     if (sr.nmF <= k) {
       if (sr.lmF != 0 && sr.lmF < m) a = newInitial(0, D_BIFWD, 0, m, sr.lmF, sr.lmF, sr.nmF);
       else a = newInitial(0, D_FORWARD, 0, m, 0, 0, sr.nmF);
-      if (a < 0) return;
+      if (a < 0) return false;
     }
     if (sr.nmR <= k) {
       if (sr.lmR != 0 && sr.lmR < m) b = newInitial(1, D_BIFWD, 0, m, sr.lmR, sr.lmR, sr.nmR);
       else b = newInitial(1, D_FORWARD, 0, m, 0, 0, sr.nmR);
-      if (b < 0) return;
+      if (b < 0) return false;
     }
     queueAdd(a);
     queueAdd(b);
-    const int upper = m * 20;
-    while (heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR) {
-      if (numFMIndexSearches > upper) break;
+    GWA_PA(PR_SEED, tsd);
+    upperSearches = m * 20;
+    return true;
+  }
+  GWA_HD int searchStep() {
+    {
+      GWA_PC(PR_NSW, PR_NSL);
+      if (!(heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR)) return SS_DONE;
+      if (numFMIndexSearches > upperSearches) return SS_DONE;
+      GWA_PT(tl);
+      GWA_PT(tp);
       const int base = queuePoll();
       // the polled state and its split chain are read once into registers
-      DState<R> B;
-      loadState(base, B);
-      tr(1, (uint32_t)base, curWord(B), (uint32_t)B.state);
+      DState<R> C;
+      loadState(base, C);
+      tr(1, (uint32_t)base, curWord(C), (uint32_t)C.state);
+      // upperBoundOfScore of the polled chain (:380), taken before the walk (which only reads)
+      const int ubScore = C.nextSplit < 0 ? stateScore(C, 0, true) : chainScore(base, true);
       int c = base;
-      DState<R> C = B;
+      GWA_PA(PR_POLL, tp);
       {
-        int reported = 0;
-        while (((((uint32_t)C.state >> 24) & 3) != 0) || cRemaining(C) == 0) {  // hasHit | isClipped | done
-          if (C.nextSplit < 0) {
-            if (!reportAlignment(base)) return;
-            reported = 1;
-            break;
-          }
+        GWA_PT(trp);
+        // skip finished members (hasHit | isClipped | done); a chain with none left is reported
+        // (single-exit loop: no break / loop-carried flag, see quickScan)
+        while (((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) && C.nextSplit >= 0) {
           c = C.nextSplit;
           loadState(c, C);
         }
-        if (reported) continue;
+        GWA_PA(PR_REPORT, trp);
+        if ((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) {
+          pendingBase = base;
+          GWA_PA(PR_LOOP, tl);
+          return SS_REPORT;
+        }
       }
-      if ((C.state & 0x1F) == 0x1F) continue;  // isFinished
+      GWA_PT(tb);
+      if ((C.state & 0x1F) == 0x1F) return SS_CONTINUE;  // isFinished
       const int nm = (int)(((uint32_t)C.state >> 8) & 0xFF);
-      if (nm > minMismatches) continue;
-      if (minMismatches - nm < 0) continue;
-      {
-        const int ub = B.nextSplit < 0 ? stateScore(B, 0, true) : chainScore(base, true);
-        if (ub < 0 || ub < bestScore) continue;
-      }
+      if (nm > minMismatches) return SS_CONTINUE;
+      if (minMismatches - nm < 0) return SS_CONTINUE;
+      if (ubScore < 0 || ubScore < bestScore) return SS_CONTINUE;
       const int strand = cStrand(C);
       const int nextBase = qcode(strand, cNextIdx(C));
-      int advanced = 0;
-      if (!(C.state & (1 << nextBase))) {
-        C.state |= 1 << nextBase;  // updateFlag
+      GWA_PA(PR_BOUND, tb);
+      GWA_PT(te);
+      // children (:386-410): nextBase first -- a state from it ends the iteration -- then every
+      // base still unchecked.  One loop, so the expansion is inlined once.
+      for (int t = -1; t < 4; ++t) {
+        const int ch = t < 0 ? nextBase : t;
+        if (C.state & (1 << ch)) continue;  // isChecked
+        C.state |= 1 << ch;                 // updateFlag
         storeStateWord(c, C.state);
-        if (!siIsEmpty(C, nextBase)) {
-          const int ns = nextStateLocal(c, C, nextBase);
-          if (ns == -2) return;
-          if (ns >= 0) { queueAdd(update(base, c, ns)); advanced = 1; }
+        if (siIsEmpty(C, ch)) continue;
+        const int ns = nextStateLocal(c, C, ch);
+        if (ns == -2) return SS_DONE;
+        if (ns >= 0) {
+          queueAdd(update(base, c, ns));
+          if (t < 0) { GWA_PA(PR_EXP1, te); GWA_PA(PR_LOOP, tl); return SS_CONTINUE; }
         }
       }
-      if (advanced) continue;
-      for (int ch = 0; ch < 4; ++ch) {
-        if (!(C.state & (1 << ch))) {
-          C.state |= 1 << ch;
-          storeStateWord(c, C.state);
-          if (!siIsEmpty(C, ch)) {
-            const int ns = nextStateLocal(c, C, ch);
-            if (ns == -2) return;
-            if (ns >= 0) queueAdd(update(base, c, ns));
-          }
-        }
-      }
+      GWA_PA(PR_EXPN, te);
+      GWA_PT(ts);
       C.state |= 1 << 4;  // updateSplitFlag
       storeStateWord(c, C.state);
       if (numSplit(base) < cfg.numSplit && nm + 1 <= minMismatches) {
         const int index = cNextIdx(C);
         if (index > cfg.indelEndSkip && m - index >= cfg.indelEndSkip) {
-          int ns = nextStateAfterSplit(c, false);
-          if (ns == -2) return;
-          if (ns >= 0) queueAdd(update(base, c, ns));
-          int cl = nextStateAfterSplit(c, true);
-          if (cl == -2) return;
-          if (cl >= 0) queueAdd(update(base, c, cl));
+          for (int clip = 0; clip < 2; ++clip) {  // split, then clip (:414-425)
+            const int ns = nextStateAfterSplit(c, clip != 0);
+            if (ns == -2) return SS_DONE;
+            if (ns >= 0) queueAdd(update(base, c, ns));
+          }
         }
       }
+      GWA_PA(PR_SPLIT, ts);
+      GWA_PA(PR_LOOP, tl);
     }
+    return SS_CONTINUE;
   }
 
   // ---- register cache of the most recently created state (the usual next poll) ----
@@ -1303,10 +1533,10 @@ struct BsfLane {
   DState<R> cache;
   GWA_HD void loadState(int idx, DState<R> &d) {
     if (idx == cacheIdx) d = cache;
-    else d = L.arena[idx];
+    else d = L.arena()[idx];
   }
   GWA_HD void storeStateWord(int idx, int32_t w) {
-    L.arena[idx].state = w;
+    L.arena()[idx].state = w;
     if (idx == cacheIdx) cache.state = w;
   }
   GWA_HD void invalidateCache() { cacheIdx = -1; }
@@ -1325,10 +1555,15 @@ struct BsfLane {
     bool hm = false;
     DState<R> d;
     d.meta = 0;
+    GWA_PT(tf);
     nextSi(cs, ch, d);  // the FM step (next(c, ch)) precedes the automaton (:422-425)
+    GWA_PA(PR_FM, tf);
     ++numFMIndexSearches;
     tr(2, (uint32_t)ch, d.lb[0] ^ (d.ub[1] * 3u) ^ (d.lb[2] * 7u) ^ (d.ub[3] * 11u) ^ d.bBase, (uint32_t)(d.meta & 3));
-    if (!nfaNext(cs, ch, strand, rows, &nh, &nko, &hm)) { tr(3, 0, 0, 0); return -1; }
+    GWA_PT(tq);
+    const bool nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm);
+    GWA_PA(PR_NFA, tq);
+    if (!nfaOk) { tr(3, 0, 0, 0); return -1; }
     tr(4, (uint32_t)nh | ((uint32_t)nko << 8) | ((uint32_t)hm << 16), (uint32_t)rows[0], (uint32_t)(nh > 1 ? rows[1] : 0));
     int id = allocState();
     if (id < 0) return -2;
@@ -1352,7 +1587,7 @@ struct BsfLane {
     d.kOffset = (uint8_t)nko;
 #pragma unroll
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
-    L.arena[id] = d;
+    L.arena()[id] = d;
     cache = d;
     cacheIdx = id;
     (void)c;
@@ -1371,6 +1606,13 @@ struct BsfLane {
     nStates = heapSize = nHits = listSize = nCigar = 0;
     cacheIdx = -1;
     status = ST_UNMAPPED;
+    stairBad = 0;
+    stairTab = nullptr;
+    if (st.base) {
+      const uint32_t b = st.base[m];
+      stairBad = b >= 0xFFFFFFFEu;
+      stairTab = (stairLds && m == st.ldsM) ? stairLds : st.tab + (stairBad ? 0 : b);
+    }
     quickSteps = blocks = saReads = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains
@@ -1391,15 +1633,15 @@ struct BsfLane {
     for (int r = 0; r < nRep; ++r) {
       oh->chainHead[r] = nh;
       int prevOut = -1;
-      for (int t = L.list[r]; t >= 0; t = L.hits[t].next) {
-        const DHit &h = L.hits[t];
+      for (int t = L.list()[r]; t >= 0; t = L.hits()[t].next) {
+        const DHit &h = L.hits()[t];
         if (nh >= outHitCap || ncg + h.cigarLen > outCigCap) { oh->status = ST_OVERFLOW; return; }
         OutHit &o = oHits[nh];
         o.chr = h.chr; o.pos = h.pos; o.matchLength = h.matchLength; o.qStart = h.qStart; o.qEnd = h.qEnd;
         o.diff = h.diff; o.strand = h.strand; o.numHits = h.numHits; o.next = -1;
         o.cigarOff = (uint16_t)ncg;
         o.cigarLen = (uint16_t)h.cigarLen;
-        for (int i = 0; i < h.cigarLen; ++i) oCig[ncg++] = L.cigar[h.cigarOff + i];
+        for (int i = 0; i < h.cigarLen; ++i) oCig[ncg++] = L.cigar()[h.cigarOff + i];
         if (prevOut >= 0) oHits[prevOut].next = nh;
         prevOut = nh;
         ++nh;

@@ -298,6 +298,7 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     sc.k = cfg->k; sc.reportType = cfg->report_type; sc.topL = cfg->top_l; sc.numSplit = cfg->num_split;
     sc.matchScore = cfg->match; sc.mismatchPenalty = cfg->mismatch; sc.splitOpenPenalty = cfg->split_open;
     sc.indelEndSkip = cfg->indel_end_skip; sc.bandWidth = cfg->band_width;
+    sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 8;
     const uint32_t n = reads->n;
     b->n = n;
     b->hasQual = reads->qual != nullptr;
@@ -343,6 +344,16 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     b->st.tab = b->d_stair;
     b->st.base = b->d_stairBase;
     b->st.kmax = std::max(b->kmax, 0);
+    b->st.ldsM = -1;
+    {  // stage the table of the longest length in LDS when it fits (all reads share it in the usual case)
+      const int km = std::max(b->kmax, 0), m0 = b->maxM;
+      const uint64_t cnt = (uint64_t)(km + 2) * (km + 1) * (uint64_t)(m0 + km + 1);
+      if (m0 >= 1 && m0 <= 255 && base[(size_t)m0] < 0xFFFFFFFEu && cnt <= (uint64_t)kStairLdsWords) {
+        b->st.ldsM = m0;
+        b->st.ldsBase = base[(size_t)m0];
+        b->st.ldsCount = (uint32_t)cnt;
+      }
+    }
     const int chains = cfg->report_type == 0 ? 1 : 4;
     b->hitCap = chains * std::max(1, cfg->num_split + 1);
     b->cigCap = 64 * chains;
@@ -418,11 +429,12 @@ int gwa_batch_run(gwa_batch_t *b) {
       const int bMax = std::max(1, (m + 63) / 64);
       const int nref = m + 2 * b->kmax + 2;
       caps.dpWords = 2 * bMax * (nref + 1);
-      caps.path = ((m + 2 * nref + 16) + 7) & ~7;
+      caps.path = m + nref + 8;
+      caps.wr = nref + 2;
       const uint64_t stride = laneBytesFor(b->R, caps);
       uint32_t lanes = std::min<uint32_t>(n, T.maxLanes);
       lanes = (lanes + 255) / 256 * 256;
-      const size_t need = (size_t)stride * lanes;
+      const size_t need = (size_t)(stride + ilvBytesFor(caps)) * lanes;
       if (need > ix->scratchBytes) {
         if (ix->scratch) HIPCHK(hipFree(ix->scratch));
         ix->scratch = nullptr;
@@ -436,9 +448,33 @@ int gwa_batch_run(gwa_batch_t *b) {
       const char *tre = getenv("GWA_TRACE_READ");
       int traceRead = tre ? atoi(tre) : -1;
       if (traceRead >= 0 && !d_trace) { HIPCHK(hipMalloc(&d_trace, 4 * 65540)); HIPCHK(hipMemset(d_trace, 0, 4 * 65540)); }
-      launchSearch(b->R, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
-                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_list[cur ^ 1], ovfCount, s,
+#ifdef GWA_PROF
+      uint64_t *d_prof = nullptr;
+      HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
+      HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
+                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
+                   (uint32_t *)d_prof, -1);
+      {
+        std::vector<uint64_t> pv((size_t)lanes * PR_N);
+        HIPCHK(hipMemcpyAsync(pv.data(), d_prof, pv.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipFree(d_prof));
+        double sum[PR_N] = {};
+        for (size_t i = 0; i < pv.size(); ++i) sum[i % PR_N] += (double)pv[i];
+        static const char *nm[PR_N] = {"poll", "report", "bound", "exp1", "add1", "expN", "split", "loop",
+                                       "verify", "nfa", "fm", "seed", "nVerifyWave", "nVerifyLane", "nStepWave",
+                                       "nStepLane", "-", "-", "-", "wave"};
+        fprintf(stderr, "[gwa-prof] tier %d reads %u lanes %u (Gcycles summed over waves; counts in M):", t, n, lanes);
+        for (int q = 0; q < PR_N; ++q)
+          if (nm[q][0] != '-') fprintf(stderr, " %s=%.2f", nm[q], sum[q] / (q >= PR_NVW && q <= PR_NSL ? 1e6 : 1e9));
+        fprintf(stderr, "\n");
+      }
+#else
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
+                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
                    traceRead >= 0 ? d_trace : nullptr, traceRead);
+#endif
       if (traceRead >= 0) {
         std::vector<uint32_t> tv(65537);
         HIPCHK(hipMemcpyAsync(tv.data(), d_trace, 4 * 65537, hipMemcpyDeviceToHost, s));

@@ -57,36 +57,114 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
   waveAppend(need, r, searchList, searchCount);
 }
 
-template <int R>
-__global__ void __launch_bounds__(256) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
+#ifndef GWA_SEARCH_WAVES
+#define GWA_SEARCH_WAVES 2
+#endif
+template <int R, int QW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES))) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
                                                          const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                                                          uint64_t laneStride, Caps caps, OutHeader *oh, OutHit *ohits,
                                                          uint16_t *ocig, int hitCap, int cigCap, const int32_t *chrRank,
-                                                         uint32_t *ovfList, uint32_t *ovfCount, uint32_t *trace, int traceRead) {
+                                                         uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *trace,
+                                                         int traceRead) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
-  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, caps);
-  // uniform trip count across the wave so the ballot in waveAppend sees every lane
-  const uint32_t rounds = (n + total - 1) / total;
-  for (uint32_t it = 0; it < rounds; ++it) {
-    const uint32_t i = gid + it * total;
+  // scratch = [lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]
+  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
+  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+#ifdef GWA_PROF
+  // profiling build: `trace` is a [lanes][PR_N] cycle-counter array, slot PR_N-1 = wave lifetime
+  uint64_t *prof = (uint64_t *)trace + (size_t)gid * PR_N;
+  const uint64_t tk = clock64();
+  trace = nullptr;
+#endif
+  __shared__ uint64_t stairLds[kStairLdsWords];
+  if (st.ldsM >= 0) {
+    for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
+    __syncthreads();
+  }
+#ifdef GWA_PERREAD_KERNEL
+  {
+    const uint32_t rounds = (n + total - 1) / total;
+    for (uint32_t it = 0; it < rounds; ++it) {
+      const uint32_t i = gid + it * total;
+      bool ovf = false;
+      uint32_t r = 0;
+      if (i < n) {
+        r = list[i];
+        const uint32_t o = reads.off[r];
+        const int m = (int)(reads.off[r + 1] - o);
+        BsfLane<R, QW> lane(ix, cfg, st, L, caps);
+        lane.chrRank = chrRank;
+        if (st.ldsM >= 0) lane.stairLds = stairLds;
+        if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
+        lane.initRead(reads.codes + o, m);
+        lane.searchPhase(sres[r]);
+        lane.writeSearchOutput(oh + r, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap, hitCap, cigCap);
+        if (lane.trace) trace[0] = (uint32_t)lane.traceN;
+        ovf = oh[r].status == ST_OVERFLOW;
+      }
+      waveAppend(ovf, r, ovfList, ovfCount);
+    }
+    return;
+  }
+#endif
+  BsfLane<R, QW> lane(ix, cfg, st, L, caps);
+  lane.chrRank = chrRank;
+  if (st.ldsM >= 0) lane.stairLds = stairLds;
+  // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
+  // the wavefront runs the parked reports (DP verification + traceback) together once they are at
+  // least half of its live lanes, instead of once per lane on a divergent path.
+  enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED };
+  int phase = IDLE;
+  uint32_t r = 0;
+  for (;;) {
+    const bool need = phase == IDLE;
+    const uint64_t needMask = __ballot(need);
+    if (needMask) {
+      const int lid = __lane_id();
+      const int leader = __ffsll((long long)needMask) - 1;
+      uint32_t base = 0;
+      if (lid == leader) base = atomicAdd(work, (uint32_t)__popcll(needMask));
+      base = __shfl(base, leader);
+      if (need) {
+        const uint64_t below = lid == 0 ? 0ULL : (needMask & ((~0ULL) >> (64 - lid)));
+        const uint32_t i = base + (uint32_t)__popcll(below);
+        if (i < n) {
+          r = list[i];
+          const uint32_t o = reads.off[r];
+          const int m = (int)(reads.off[r + 1] - o);
+          lane.trace = nullptr;
+          if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; lane.traceN = 0; }
+          lane.initRead(reads.codes + o, m);
+          phase = lane.searchStart(sres[r]) ? RUN : FINISH;
+        } else {
+          phase = EXHAUSTED;
+        }
+      }
+    }
+    if (__ballot(phase != EXHAUSTED) == 0) break;
+    const int nWait = __popcll(__ballot(phase == WAIT));
+    const int nRun = __popcll(__ballot(phase == RUN));
+    if (nWait > 0 && nWait * 16 >= cfg.waitQ16 * (nWait + nRun)) {
+      if (phase == WAIT) phase = lane.searchReport() ? RUN : FINISH;
+    } else if (phase == RUN) {
+      const int sst = lane.searchStep();
+      phase = sst == BsfLane<R, QW>::SS_REPORT ? WAIT : sst == BsfLane<R, QW>::SS_DONE ? FINISH : RUN;
+    }
     bool ovf = false;
-    uint32_t r = 0;
-    if (i < n) {
-      r = list[i];
-      const uint32_t o = reads.off[r];
-      const int m = (int)(reads.off[r + 1] - o);
-      BsfLane<R> lane(ix, cfg, st, L, caps);
-      lane.chrRank = chrRank;
-      if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
-      lane.initRead(reads.codes + o, m);
-      lane.searchPhase(sres[r]);
+    if (phase == FINISH) {
       lane.writeSearchOutput(oh + r, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap, hitCap, cigCap);
       if (lane.trace) trace[0] = (uint32_t)lane.traceN;
       ovf = oh[r].status == ST_OVERFLOW;
+      phase = IDLE;
     }
     waveAppend(ovf, r, ovfList, ovfCount);
   }
+#ifdef GWA_PROF
+  for (int q = 0; q < PR_N - 1; ++q) prof[q] += lane.prof[q];
+  if (__lane_id() == 0) prof[PR_N - 1] += clock64() - tk;
+#endif
 }
 
 void launchQuickscan(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
@@ -98,23 +176,29 @@ void launchQuickscan(const IndexView &ix, const SearchConfig &cfg, const ReadsVi
                      searchList, searchCount, trace, traceRead);
 }
 
-void launchSearch(int R, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+void launchSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                   uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
-                  const int32_t *chrRank, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s, uint32_t *trace,
-                  int traceRead) {
+                  const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s,
+                  uint32_t *trace, int traceRead) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
-  switch (R) {
-#define GWA_CASE(RR)                                                                                                  \
-  case RR:                                                                                                            \
-    hipLaunchKernelGGL(bsf_search_kernel<RR>, grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n, scratch,     \
-                       laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, ovfList, ovfCount, trace, traceRead);                \
+  const int key = R * 16 + QW;
+  switch (key) {
+#define GWA_CASE(RR, QQ)                                                                                              \
+  case RR * 16 + QQ:                                                                                                  \
+    hipLaunchKernelGGL((bsf_search_kernel<RR, QQ>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n, scratch, \
+                       laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, work, ovfList, ovfCount, trace,     \
+                       traceRead);                                                                                    \
     break;
-    GWA_CASE(4)
-    GWA_CASE(8)
-    GWA_CASE(16)
-    GWA_CASE(32)
+    GWA_CASE(4, 4)
+    GWA_CASE(4, 8)
+    GWA_CASE(8, 4)
+    GWA_CASE(8, 8)
+    GWA_CASE(16, 4)
+    GWA_CASE(16, 8)
+    GWA_CASE(32, 4)
+    GWA_CASE(32, 8)
 #undef GWA_CASE
     default: break;
   }
@@ -128,5 +212,6 @@ size_t laneBytesFor(int R, const Caps &c) {
     default: return laneBytes<32>(c);
   }
 }
+size_t ilvBytesFor(const Caps &c) { return ilvBytes(c); }
 
 }  // namespace gwa

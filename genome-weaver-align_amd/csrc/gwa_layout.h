@@ -57,6 +57,9 @@ struct SearchConfig {
   int32_t numSplit;
   int32_t matchScore, mismatchPenalty, splitOpenPenalty;
   int32_t indelEndSkip, bandWidth;
+  // scheduler (not a reference option): a wavefront runs its parked reports once they are at least
+  // waitQ16/16 of its live lanes
+  int32_t waitQ16;
 };
 
 // Read batch as resident in HBM: 2-bit-per-byte codes (0..4) per read, concatenated.
@@ -73,8 +76,10 @@ struct StairTables {
   const uint64_t *tab;
   const uint32_t *base;  // per m (0..255), index into tab; 0xFFFFFFFF = no table
   int32_t kmax;
-  int32_t pad;
+  int32_t ldsM;          // reads of this length use a copy of their table staged in LDS (-1 = none)
+  uint32_t ldsBase, ldsCount;  // that table: tab[ldsBase, ldsBase + ldsCount)
 };
+constexpr int kStairLdsWords = 2048;  // 16 KiB of LDS per workgroup
 
 // ---- per-read output ----
 enum : int32_t {
@@ -116,4 +121,7 @@ struct ScanRes {
 };
 
 // CIGAR op = (len << 3) | type ; type: M0 I1 D2 N3 S4 H5 P6 X7  (A/CIGAR.java:39-47)
+// search-loop profiling regions (-DGWA_PROF builds)
+enum { PR_POLL, PR_REPORT, PR_BOUND, PR_EXP1, PR_ADD1, PR_EXPN, PR_SPLIT, PR_LOOP, PR_VERIFY, PR_NFA, PR_FM, PR_SEED, PR_NVW, PR_NVL, PR_NSW, PR_NSL, PR_N = 20 };
+
 }  // namespace gwa

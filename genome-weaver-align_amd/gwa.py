@@ -13,7 +13,7 @@ import os
 from dataclasses import dataclass, fields
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(_HERE, "libgwa.so")
+LIBPATH = os.path.join(_HERE, os.environ.get("GWA_LIB", "libgwa.so"))  # GWA_LIB=libgwa_prof.so: profiling build
 
 
 class GwaError(RuntimeError):

@@ -20,15 +20,15 @@ struct HC {
 };
 
 // the GPU's capacity tiers (gwa_api.cpp kTiers) replayed on the CPU
-template <int R>
+template <int R, int QW>
 static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int maxM, int kmax, uint32_t n,
                   const char *const *names, const char *const *seqs, const char *const *quals, std::string &sam,
                   int32_t *stats) {
   const int bMax = std::max(1, (maxM + 63) / 64), nref = maxM + 2 * kmax + 2;
-  const int dpw = 2 * bMax * (nref + 1), path = ((maxM + 2 * nref + 16) + 7) & ~7;
-  const Caps tiers[3] = {{256, 256, 32, 32, 512, dpw, path}, {4096, 4096, 256, 256, 4096, dpw, path},
-                         {65536, 65536, 4096, 4096, 65536, dpw, path}};
-  std::vector<uint8_t> scratch(laneBytes<R>(tiers[2]) + 4096);
+  const int dpw = 2 * bMax * (nref + 1), path = maxM + nref + 8, wrn = nref + 2;
+  const Caps tiers[3] = {{256, 256, 32, 32, 512, dpw, path, wrn}, {4096, 4096, 256, 256, 4096, dpw, path, wrn},
+                         {65536, 65536, 4096, 4096, 65536, dpw, path, wrn}};
+  std::vector<uint8_t> scratch(laneBytes<R>(tiers[2]) + ilvBytes(tiers[2]) + 4096);
   const int chains = cfg.reportType == 0 ? 1 : 4;
   const int hitCap = chains * (cfg.numSplit + 1), cigCap = 64 * chains;
   std::vector<OutHit> oh(hitCap);
@@ -43,7 +43,7 @@ static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int max
     bool traced = false;
     for (int t = 0; t < 3; ++t) {
       LaneMem<R> L = laneMem<R>(scratch.data(), tiers[t]);
-      BsfLane<R> lane(x->v, cfg, st, L, tiers[t]);
+      BsfLane<R, QW> lane(x->v, cfg, st, L, tiers[t]);
       lane.chrRank = rk.data();
       const char *tre = getenv("GWA_TRACE_READ");
       const char *qtre = getenv("GWA_QTRACE_READ");
@@ -135,17 +135,17 @@ int hc_align(void *p, float k, int reportType, int numSplit, uint32_t n, const c
   std::vector<uint64_t> tab;
   std::vector<uint32_t> base;
   buildStairTables(lens, kmax, tab, base);
-  StairTables st{tab.data(), base.data(), kmax, 0};
+  StairTables st{tab.data(), base.data(), kmax, -1, 0, 0};
   std::string sam;
   int maxM = 1;
   for (int m : lens) maxM = std::max(maxM, m);
   int R = kmax + 1 <= 4 ? 4 : kmax + 1 <= 8 ? 8 : kmax + 1 <= 16 ? 16 : 32;
   int rc = 0;
   switch (R) {
-    case 4: rc = runAll<4>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    case 8: rc = runAll<8>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    case 16: rc = runAll<16>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    default: rc = runAll<32>(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 4: rc = (maxM <= 128 ? runAll<4, 4> : runAll<4, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 8: rc = (maxM <= 128 ? runAll<8, 4> : runAll<8, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 16: rc = (maxM <= 128 ? runAll<16, 4> : runAll<16, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    default: rc = (maxM <= 128 ? runAll<32, 4> : runAll<32, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
   }
   if (rc != 0) return rc;
   *out = (char *)malloc(sam.size() + 1);
