@@ -1,5 +1,5 @@
 #include <hip/hip_runtime.h>
-#include "bsf_core.h"
+#include "../genome-weaver-align_amd/csrc/bsf_core.h"
 using namespace gwa;
 template <int V>
 __global__ void __launch_bounds__(256) probe(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const ScanRes *sres,
