@@ -40,6 +40,7 @@ def main():
     import numpy as np
     import synth
     import gwa
+    import dist as gdist
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -104,11 +105,7 @@ def main():
         sms += st.search_ms
     torch.cuda.synchronize()
     barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt])
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t[0])
+    dt = gdist.max_over_ranks(time.perf_counter() - t0)
 
     nres = min(args.check, reads_per_step)
     sam, off = batch.results(0, nres)

@@ -1,0 +1,45 @@
+"""Read sharding across GPUs of one node: replicas only, no data-path collective.
+
+Every rank holds a full index replica in its own HBM and aligns a contiguous shard of the read
+batch; the only communication is (i) the max-over-ranks elapsed time for the benchmark and
+(ii) an optional gather of SAM text to rank 0, concatenated in rank order so the merged output
+is byte-identical to a single-GPU run (the reference emits in input order, A/Align.java:187-195).
+Works with any torch.distributed backend (gloo on CPU in tests, nccl=RCCL on the GPU box).
+"""
+import os
+
+
+def world():
+    """(rank, world_size, local_rank) from the torchrun environment; (0, 1, 0) standalone."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_bounds(n, rank, world_size):
+    """Contiguous shard [lo, hi) of n reads for `rank`; shard sizes differ by at most one."""
+    if world_size < 1 or not 0 <= rank < world_size:
+        raise ValueError("bad rank %d / world %d" % (rank, world_size))
+    q, r = divmod(n, world_size)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def max_over_ranks(value):
+    """Max of a float over all ranks (the benchmark's step time); identity when not distributed."""
+    import torch
+    import torch.distributed as td
+    if not (td.is_available() and td.is_initialized()) or td.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    td.all_reduce(t, op=td.ReduceOp.MAX)
+    return float(t[0])
+
+
+def gather_sam(sam_text, dst=0):
+    """Gather each rank's SAM text to `dst`, concatenated in rank order (None on other ranks)."""
+    import torch.distributed as td
+    if not (td.is_available() and td.is_initialized()) or td.get_world_size() == 1:
+        return sam_text
+    parts = [None] * td.get_world_size() if td.get_rank() == dst else None
+    td.gather_object(sam_text, parts, dst=dst)
+    return "".join(parts) if td.get_rank() == dst else None
