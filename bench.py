@@ -24,6 +24,24 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def _pmc_traffic(kernel, workload):
+    """Per-launch HBM read bytes of `kernel` from the newest committed rocprofv3 PMC summary of the
+    same workload (profiles/*_profile.json, written by tools/prof_summary.py from FETCH_SIZE with
+    the guide's gfx950 x2 correction); (None, None) when no profile of this workload exists."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_profile.json")), key=os.path.getmtime):
+        try:
+            d = json.load(open(f))
+            line = d.get("bench_lines", {}).get("bench.json", {})
+            k = d["kernels"][kernel + "_kernel"]
+        except (OSError, ValueError, KeyError):
+            continue
+        if line.get("config", {}).get("workload") == workload and "hbm_read_bytes_corrected" in k:
+            best = (k["hbm_read_bytes_corrected"], os.path.relpath(f, REPO))
+    return best if best else (None, None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,16 +170,18 @@ def main():
     else:
         dom, ach_bytes, dom_ms = "bsf_search", s_bytes, s_ms
     achieved = ach_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    workload = ("%s; %d x 100 bp reads per GPU per step, 0-2 substitutions, -k %g, -m bsf, besthit"
+                % (gname, reads_per_step, args.k))
+    traffic, traffic_src = _pmc_traffic(dom, workload)
     out = {
         "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-        "config": {"workload": "%s; %d x 100 bp reads per GPU per step, 0-2 substitutions, -k %g, -m bsf, besthit"
-                               % (gname, reads_per_step, args.k),
+        "config": {"workload": workload,
                    "genome_bp": int(len(codes)), "reads_per_gpu_per_step": reads_per_step,
                    "parallelism": "reads sharded, index replicated (%d GPU)" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": ach_bytes, "avg_launch_ms": dom_ms},
         "cpu_baseline": cpu,
         "detail": {"quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,

@@ -1,0 +1,96 @@
+"""Summarise a tools/profile.sh run (rocprofv3 kernel trace + PMC passes) into one JSON file.
+
+  python tools/prof_summary.py gpurun_out/prof_<tag> profiles/<round>_<tag>.json
+
+Per kernel of the align path: dispatch count, average duration (kernel trace), and per-dispatch
+PMC averages.  FETCH_SIZE is rocprofv3's derived memory-side read volume in KiB; per
+/opt/skills/guides/MI355X_MICROARCH.md (§HBM) gfx950 reports half the bytes of 16-B-per-lane
+reads, so `hbm_read_bytes_corrected` = 2 x 1024 x FETCH_SIZE.  Infinity-Cache hits are counted
+in FETCH_SIZE (guide), so this is an upper bound on HBM traffic.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNELS = ["fm_quickscan_kernel", "bsf_search_kernel"]
+
+
+def _short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
+
+def _rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def summarise(d):
+    res = {"kernels": {}}
+    # kernel trace: durations
+    for r in _rows(os.path.join(d, "trace", "**", "*_kernel_trace.csv")):
+        k = _short(r["Kernel_Name"])
+        if not k:
+            continue
+        e = res["kernels"].setdefault(k, {"dispatches": 0, "durations_ns": []})
+        e["dispatches"] += 1
+        e["durations_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        e["vgpr"] = int(r.get("VGPR_Count") or 0)
+        e["agpr"] = int(r.get("Accum_VGPR_Count") or 0)
+        e["lds_bytes"] = int(r.get("LDS_Block_Size") or 0)
+        e["scratch_bytes"] = int(r.get("Scratch_Size") or 0)
+    for k, e in res["kernels"].items():
+        ds = e.pop("durations_ns")
+        e["avg_ms"] = sum(ds) / len(ds) / 1e6
+        e["min_ms"] = min(ds) / 1e6
+        e["max_ms"] = max(ds) / 1e6
+    # PMC passes: average per dispatch of each counter
+    for sub in ["pmc_fetch", "pmc_sq", "pmc_tcc"]:
+        acc = {}
+        for r in _rows(os.path.join(d, sub, "**", "*_counter_collection.csv")):
+            k = _short(r["Kernel_Name"])
+            if not k:
+                continue
+            key = (k, r["Dispatch_Id"], r["Counter_Name"])
+            acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
+        per = {}
+        for (k, disp, cn), v in acc.items():
+            per.setdefault((k, cn), []).append(v)
+        for (k, cn), vs in per.items():
+            e = res["kernels"].setdefault(k, {})
+            e.setdefault("pmc", {})[cn] = sum(vs) / len(vs)
+    for k, e in res["kernels"].items():
+        p = e.get("pmc", {})
+        if "FETCH_SIZE" in p:
+            e["hbm_read_bytes_corrected"] = 2.0 * 1024.0 * p["FETCH_SIZE"]
+        if "TCC_HIT_sum" in p and "TCC_MISS_sum" in p and p["TCC_HIT_sum"] + p["TCC_MISS_sum"] > 0:
+            e["l2_hit_rate"] = p["TCC_HIT_sum"] / (p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
+        if "SQ_WAIT_ANY" in p and p.get("SQ_WAVE_CYCLES"):
+            e["wait_frac"] = p["SQ_WAIT_ANY"] / p["SQ_WAVE_CYCLES"]
+    for name in ["bench.json", "bench_pmc1.json"]:
+        f = os.path.join(d, name)
+        if os.path.exists(f) and os.path.getsize(f):
+            with open(f) as fh:
+                res.setdefault("bench_lines", {})[name] = json.loads(fh.read().strip().splitlines()[-1])
+    stats = glob.glob(os.path.join(d, "trace", "**", "*_kernel_stats.csv"), recursive=True)
+    if stats:
+        with open(stats[0]) as fh:
+            res["kernel_stats_csv"] = fh.read()
+    return res
+
+
+if __name__ == "__main__":
+    out = summarise(sys.argv[1])
+    txt = json.dumps(out, indent=1, sort_keys=True)
+    if len(sys.argv) > 2:
+        with open(sys.argv[2], "w") as f:
+            f.write(txt + "\n")
+    for k, e in out["kernels"].items():
+        print(k, {x: e[x] for x in e if x != "pmc"}, e.get("pmc"))
