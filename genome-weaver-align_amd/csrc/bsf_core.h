@@ -52,6 +52,13 @@ GWA_HD T pinv(T x) {
 #define GWA_PC(w, l)
 #endif
 
+// LDS-typed pointer on the device (plain pointer on host builds)
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) const uint64_t lds_cu64;
+#else
+typedef const uint64_t lds_cu64;
+#endif
+
 template <class T, int N>
 GWA_HD T pick(const T (&a)[N], int i) {
   T v = pinv(a[0]);
@@ -167,8 +174,12 @@ struct LaneMem {
   uint32_t oHeap, oHits, oList, oCigar;  // byte offsets in the slice
   uint32_t oWr, oPath;     // byte offsets of the wr / path planes in the chunk
   int lane, is;            // lane in the interleaved block, interleave stride (elements)
+  // PriorityQueue array of (key << 16 | state index): entry i at heapP[i * hs].  In the slice
+  // (hs = 1) or, for the first tier, in LDS interleaved across the workgroup (hs = 256)
+  uint64_t *heapP;
+  int hs;
   GWA_HD DState<R> *arena() const { return (DState<R> *)slice; }
-  GWA_HD uint64_t *heap() const { return (uint64_t *)(slice + oHeap); }  // PriorityQueue array of (key << 16 | state index)
+  GWA_HD uint64_t *heap() const { return heapP; }
   GWA_HD DHit *hits() const { return (DHit *)(slice + oHits); }
   GWA_HD int32_t *list() const { return (int32_t *)(slice + oList); }
   GWA_HD uint16_t *cigar() const { return (uint16_t *)(slice + oCigar); }
@@ -207,6 +218,8 @@ GWA_HD LaneMem<R> laneMem(uint8_t *slice, uint8_t *chunk, int laneInWave, int is
   L.oPath = (uint32_t)((size_t)is * (8 * (size_t)c.dpWords + (size_t)c.wr));
   L.lane = laneInWave;
   L.is = is;
+  L.heapP = (uint64_t *)(slice + L.oHeap);
+  L.hs = 1;
   return L;
 }
 template <int R>
@@ -269,7 +282,7 @@ struct BsfLane {
   int nStates, heapSize, nHits, listSize, nCigar;
   int status;  // ST_*
   // instrumentation
-  int quickSteps, blocks, saReads;
+  int quickSteps, blocks, saReads, maxHeap;
   // debug trace (nullptr in production launches): 4 words per event
   uint32_t *trace = nullptr;
   int traceCap = 0, traceN = 0;
@@ -417,16 +430,21 @@ struct BsfLane {
     return p;
   }
   // StaircaseFilter.getStairCaseMask64bit via the host-built table (S/StaircaseFilter.java:91-102)
-  // this read's table (resolved once per read in initRead; LDS when the kernel staged it)
-  const uint64_t *stairLds = nullptr;
+  // this read's table (resolved once per read in initRead): the LDS copy when the kernel staged
+  // the table of this length, else global memory.  The LDS pointer is typed address_space(3) so
+  // the two loads are never merged into one flat load (which would wait on every outstanding
+  // global access).
+  lds_cu64 *stairLds = nullptr;
   const uint64_t *stairTab = nullptr;
-  int stairBad = 0;
+  int stairBad = 0, stairInLds = 0;
   GWA_HD int64_t stairMask(int row, int offset) {
     const int kk = minMismatches;
     if (row >= kk + 1) return 0;
     const int km = st.kmax;
     if (stairBad) { status = ST_ERROR; return 0; }  // StaircaseFilter ctor throws for this m
-    return (int64_t)stairTab[(size_t)(kk * (km + 1) + row) * (size_t)(m + km + 1) + (size_t)(offset + km)];
+    const size_t i = (size_t)(kk * (km + 1) + row) * (size_t)(m + km + 1) + (size_t)(offset + km);
+    if (stairInLds) return (int64_t)stairLds[i];
+    return (int64_t)stairTab[i];
   }
 
   // ---- Cursor (S/Cursor.java) ----
@@ -569,31 +587,17 @@ struct BsfLane {
   }
   GWA_HD void refreshKeys() {
     for (int i = 0; i < heapSize; ++i) {
-      const int idx = (int)(L.heap()[i] & 0xFFFF);
-      L.heap()[i] = (keyOf(idx) << 16) | (uint64_t)idx;
+      const int idx = (int)(L.heap()[(size_t)(i) * L.hs] & 0xFFFF);
+      L.heap()[(size_t)(i) * L.hs] = (keyOf(idx) << 16) | (uint64_t)idx;
     }
   }
   // java.util.PriorityQueue.offer / poll on cached keys.  The element moves are exactly Java's
   // siftUp / siftDown; only the loads are reordered: offer reads the whole ancestor path (up to
   // 8 levels) at once, poll reads children and grandchildren together, so a heap operation waits
   // on memory once per 8 (offer) or 2 (poll) levels instead of once per level.
-#ifdef GWA_SIMPLE_ADD
   GWA_HD void queueAddKeyed(uint64_t e) {
     if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
-    int kk = heapSize++;
-    const uint64_t ek = e >> 16;
-    while (kk > 0) {
-      int parent = (kk - 1) >> 1;
-      uint64_t p = L.heap()[parent];
-      if (ek >= (p >> 16)) break;
-      L.heap()[kk] = p;
-      kk = parent;
-    }
-    L.heap()[kk] = e;
-  }
-#else
-  GWA_HD void queueAddKeyed(uint64_t e) {
-    if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
+    maxHeap = heapSize + 1 > maxHeap ? heapSize + 1 : maxHeap;
     const int kk = heapSize++;
     const uint64_t ek = e >> 16;
     constexpr int MAXD = 8;
@@ -605,7 +609,7 @@ struct BsfLane {
       for (int d = 0; d < MAXD; ++d) {
         const int p = idx > 0 ? (idx - 1) >> 1 : 0;
         ai[d] = p;
-        av[d] = L.heap()[p];
+        av[d] = L.heap()[(size_t)(p) * L.hs];
         idx = p;
       }
     }
@@ -618,52 +622,25 @@ struct BsfLane {
     for (int d = MAXD - 1; d >= 0; --d) t = (d >= depth || ek >= (av[d] >> 16)) ? d : t;
 #pragma unroll
     for (int d = 0; d < MAXD; ++d)
-      if (d < t) L.heap()[d == 0 ? kk : ai[d - 1]] = av[d];
+      if (d < t) L.heap()[(size_t)(d == 0 ? kk : ai[d - 1]) * L.hs] = av[d];
     int pos = t == 0 ? kk : pick(ai, t - 1);
     if (t == MAXD) {  // deeper than MAXD levels (large tiers only): Java's loop from there
       while (pos > 0) {
         const int parent = (pos - 1) >> 1;
-        const uint64_t p = L.heap()[parent];
+        const uint64_t p = L.heap()[(size_t)(parent) * L.hs];
         if (ek >= (p >> 16)) break;
-        L.heap()[pos] = p;
+        L.heap()[(size_t)(pos) * L.hs] = p;
         pos = parent;
       }
     }
-    L.heap()[pos] = e;
+    L.heap()[(size_t)(pos) * L.hs] = e;
     tr(9, (uint32_t)(e & 0xFFFF), (uint32_t)kk, (uint32_t)pos);
   }
-#endif
-#ifdef GWA_SIMPLE_POLL
   GWA_HD int queuePoll() {
     if (heapSize == 0) return -1;
     int s = --heapSize;
-    const uint64_t result = L.heap()[0];
-    const uint64_t x = L.heap()[s];
-    if (s != 0) {
-      int kk = 0, half = heapSize >> 1;
-      const uint64_t xk = x >> 16;
-      while (kk < half) {
-        int child = (kk << 1) + 1;
-        uint64_t c = L.heap()[child];
-        int right = child + 1;
-        if (right < heapSize) {
-          uint64_t rc = L.heap()[right];
-          if ((c >> 16) > (rc >> 16)) { c = rc; child = right; }
-        }
-        if (xk <= (c >> 16)) break;
-        L.heap()[kk] = c;
-        kk = child;
-      }
-      L.heap()[kk] = x;
-    }
-    return (int)(result & 0xFFFF);
-  }
-#else
-  GWA_HD int queuePoll() {
-    if (heapSize == 0) return -1;
-    int s = --heapSize;
-    const uint64_t result = L.heap()[0];
-    const uint64_t x = L.heap()[s];
+    const uint64_t result = L.heap()[(size_t)(0) * L.hs];
+    const uint64_t x = L.heap()[(size_t)(s) * L.hs];
     if (s != 0) {
       const int n = heapSize, half = n >> 1, capm1 = caps.heap - 1;
       int kk = 0;
@@ -674,16 +651,16 @@ struct BsfLane {
         // at or past n are never selected)
         const int c = (kk << 1) + 1;
         const int g = (kk << 2) + 3;
-        const uint64_t c0 = L.heap()[c], c1 = L.heap()[c + 1 <= capm1 ? c + 1 : capm1];
-        const uint64_t g0 = L.heap()[g <= capm1 ? g : capm1], g1 = L.heap()[g + 1 <= capm1 ? g + 1 : capm1];
-        const uint64_t g2 = L.heap()[g + 2 <= capm1 ? g + 2 : capm1], g3 = L.heap()[g + 3 <= capm1 ? g + 3 : capm1];
+        const uint64_t c0 = L.heap()[(size_t)(c) * L.hs], c1 = L.heap()[(size_t)(c + 1 <= capm1 ? c + 1 : capm1) * L.hs];
+        const uint64_t g0 = L.heap()[(size_t)(g <= capm1 ? g : capm1) * L.hs], g1 = L.heap()[(size_t)(g + 1 <= capm1 ? g + 1 : capm1) * L.hs];
+        const uint64_t g2 = L.heap()[(size_t)(g + 2 <= capm1 ? g + 2 : capm1) * L.hs], g3 = L.heap()[(size_t)(g + 3 <= capm1 ? g + 3 : capm1) * L.hs];
         // level 1
         const int right = (c + 1 < n && (c0 >> 16) > (c1 >> 16)) ? 1 : 0;
         const uint64_t cv = right ? c1 : c0;
         if (xk <= (cv >> 16)) {
           go = 0;
         } else {
-          L.heap()[kk] = cv;
+          L.heap()[(size_t)(kk) * L.hs] = cv;
           kk = c + right;
           go = kk < half;
         }
@@ -696,18 +673,17 @@ struct BsfLane {
           if (xk <= (dv >> 16)) {
             go = 0;
           } else {
-            L.heap()[kk] = dv;
+            L.heap()[(size_t)(kk) * L.hs] = dv;
             kk = c2 + right2;
             go = kk < half;
           }
         }
       }
-      L.heap()[kk] = x;
+      L.heap()[(size_t)(kk) * L.hs] = x;
     }
     tr(10, (uint32_t)(result & 0xFFFF), (uint32_t)heapSize, (uint32_t)(x & 0xFFFF));
     return (int)(result & 0xFFFF);
   }
-#endif
   GWA_HD void queueAdd(int e) {
     if (e < 0) return;
     queueAddKeyed((keyOf(e) << 16) | (uint64_t)e);
@@ -1607,13 +1583,15 @@ struct BsfLane {
     cacheIdx = -1;
     status = ST_UNMAPPED;
     stairBad = 0;
+    stairInLds = 0;
     stairTab = nullptr;
     if (st.base) {
       const uint32_t b = st.base[m];
       stairBad = b >= 0xFFFFFFFEu;
-      stairTab = (stairLds && m == st.ldsM) ? stairLds : st.tab + (stairBad ? 0 : b);
+      stairInLds = (stairLds != nullptr && m == st.ldsM) ? 1 : 0;
+      stairTab = st.tab + (stairBad ? 0 : b);
     }
-    quickSteps = blocks = saReads = 0;
+    quickSteps = blocks = saReads = maxHeap = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains
   GWA_HD void writeSearchOutput(OutHeader *oh, OutHit *oHits, uint16_t *oCig, int outHitCap, int outCigCap) {
@@ -1621,6 +1599,7 @@ struct BsfLane {
     oh->searchBlocks = blocks;
     oh->saReads = saReads;
     oh->states = nStates;
+    oh->maxHeap = maxHeap;
     oh->nChains = 0;
     oh->nHits = 0;
     oh->nCigar = 0;

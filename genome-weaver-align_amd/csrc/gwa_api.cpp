@@ -380,7 +380,7 @@ struct Tier {
   uint32_t maxLanes;
 };
 static const Tier kTiers[3] = {
-    {256, 256, 32, 32, 512, 256u * 1024u},
+    {256, kLdsHeap, 32, 32, 512, 256u * 1024u},  // heap in LDS
     {4096, 4096, 256, 256, 4096, 16384u},
     {65536, 65536, 4096, 4096, 65536, 1024u},
 };
@@ -452,7 +452,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
                    b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
                    (uint32_t *)d_prof, -1);
       {
@@ -471,7 +471,7 @@ int gwa_batch_run(gwa_batch_t *b) {
         fprintf(stderr, "\n");
       }
 #else
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
                    b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
                    traceRead >= 0 ? d_trace : nullptr, traceRead);
 #endif

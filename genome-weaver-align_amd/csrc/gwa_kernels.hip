@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
 #ifndef GWA_SEARCH_WAVES
 #define GWA_SEARCH_WAVES 2
 #endif
-template <int R, int QW>
+template <int R, int QW, int LH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES))) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
                                                          const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                                                          uint64_t laneStride, Caps caps, OutHeader *oh, OutHit *ohits,
@@ -72,6 +72,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   // scratch = [lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]
   uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
   LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+  // first tier: the priority queue lives in LDS, entry i of thread t at heapLds[i * 256 + t]
+  // (heap high-water marks are ~5 entries for k <= 2, 100 bp; larger heaps overflow to tier 1)
+  __shared__ uint64_t heapLds[LH ? kLdsHeap * 256 : 1];
+  if (LH) {
+    L.heapP = heapLds + threadIdx.x;
+    L.hs = 256;
+  }
 #ifdef GWA_PROF
   // profiling build: `trace` is a [lanes][PR_N] cycle-counter array, slot PR_N-1 = wave lifetime
   uint64_t *prof = (uint64_t *)trace + (size_t)gid * PR_N;
@@ -96,7 +103,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
         const int m = (int)(reads.off[r + 1] - o);
         BsfLane<R, QW> lane(ix, cfg, st, L, caps);
         lane.chrRank = chrRank;
-        if (st.ldsM >= 0) lane.stairLds = stairLds;
+        if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
         if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
         lane.initRead(reads.codes + o, m);
         lane.searchPhase(sres[r]);
@@ -111,7 +118,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 #endif
   BsfLane<R, QW> lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
-  if (st.ldsM >= 0) lane.stairLds = stairLds;
+  if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
   // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
   // the wavefront runs the parked reports (DP verification + traceback) together once they are at
   // least half of its live lanes, instead of once per lane on a divergent path.
@@ -176,29 +183,31 @@ void launchQuickscan(const IndexView &ix, const SearchConfig &cfg, const ReadsVi
                      searchList, searchCount, trace, traceRead);
 }
 
-void launchSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
-                  const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
-                  uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
-                  const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s,
-                  uint32_t *trace, int traceRead) {
+void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,
+                  const StairTables &st, const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n,
+                  uint8_t *scratch, uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig,
+                  int hitCap, int cigCap, const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
+                  hipStream_t s, uint32_t *trace, int traceRead) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
-  const int key = R * 16 + QW;
+  const int key = (R * 16 + QW) * 2 + (ldsHeap ? 1 : 0);
   switch (key) {
-#define GWA_CASE(RR, QQ)                                                                                              \
-  case RR * 16 + QQ:                                                                                                  \
-    hipLaunchKernelGGL((bsf_search_kernel<RR, QQ>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n, scratch, \
-                       laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, work, ovfList, ovfCount, trace,     \
-                       traceRead);                                                                                    \
+#define GWA_CASE(RR, QQ, LL)                                                                                          \
+  case (RR * 16 + QQ) * 2 + LL:                                                                                       \
+    hipLaunchKernelGGL((bsf_search_kernel<RR, QQ, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
+                       scratch, laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, work, ovfList, ovfCount,  \
+                       trace, traceRead);                                                                             \
     break;
-    GWA_CASE(4, 4)
-    GWA_CASE(4, 8)
-    GWA_CASE(8, 4)
-    GWA_CASE(8, 8)
-    GWA_CASE(16, 4)
-    GWA_CASE(16, 8)
-    GWA_CASE(32, 4)
-    GWA_CASE(32, 8)
+#define GWA_CASE2(RR, QQ) GWA_CASE(RR, QQ, 0) GWA_CASE(RR, QQ, 1)
+    GWA_CASE2(4, 4)
+    GWA_CASE2(4, 8)
+    GWA_CASE2(8, 4)
+    GWA_CASE2(8, 8)
+    GWA_CASE2(16, 4)
+    GWA_CASE2(16, 8)
+    GWA_CASE2(32, 4)
+    GWA_CASE2(32, 8)
+#undef GWA_CASE2
 #undef GWA_CASE
     default: break;
   }

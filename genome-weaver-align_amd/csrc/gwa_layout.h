@@ -80,6 +80,7 @@ struct StairTables {
   uint32_t ldsBase, ldsCount;  // that table: tab[ldsBase, ldsBase + ldsCount)
 };
 constexpr int kStairLdsWords = 2048;  // 16 KiB of LDS per workgroup
+constexpr int kLdsHeap = 16;          // first-tier priority-queue capacity (entries, in LDS)
 
 // ---- per-read output ----
 enum : int32_t {
@@ -111,7 +112,7 @@ struct OutHeader {
   int32_t chainHead[4];
   // instrumentation: FM steps, quick-scan steps, rank block loads
   int32_t fmSearches, quickSteps, blocks, states;
-  int32_t searchBlocks, saReads, pad0, pad1;
+  int32_t searchBlocks, saReads, maxHeap, pad1;  // maxHeap: heap high-water mark (instrumentation)
 };
 
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at

@@ -26,7 +26,7 @@ static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int max
                   int32_t *stats) {
   const int bMax = std::max(1, (maxM + 63) / 64), nref = maxM + 2 * kmax + 2;
   const int dpw = 2 * bMax * (nref + 1), path = maxM + nref + 8, wrn = nref + 2;
-  const Caps tiers[3] = {{256, 256, 32, 32, 512, dpw, path, wrn}, {4096, 4096, 256, 256, 4096, dpw, path, wrn},
+  const Caps tiers[3] = {{256, kLdsHeap, 32, 32, 512, dpw, path, wrn}, {4096, 4096, 256, 256, 4096, dpw, path, wrn},
                          {65536, 65536, 4096, 4096, 65536, dpw, path, wrn}};
   std::vector<uint8_t> scratch(laneBytes<R>(tiers[2]) + ilvBytes(tiers[2]) + 4096);
   const int chains = cfg.reportType == 0 ? 1 : 4;
@@ -61,7 +61,7 @@ static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int max
       FILE *tf = fopen("hc_trace.bin", "wb");
       if (tf) { fwrite(tv.data(), 4, 1 + tv[0], tf); fclose(tf); }
     }
-    if (stats) { stats[i * 4] = hd.fmSearches; stats[i * 4 + 1] = hd.quickSteps; stats[i * 4 + 2] = hd.searchBlocks; stats[i * 4 + 3] = hd.states; }
+    if (stats) { stats[i * 4] = hd.fmSearches; stats[i * 4 + 1] = hd.quickSteps; stats[i * 4 + 2] = hd.maxHeap; stats[i * 4 + 3] = hd.states; }
     ReadText rt{names[i], strlen(names[i]), seqs[i], strlen(seqs[i]), quals ? quals[i] : nullptr, (quals && quals[i]) ? strlen(quals[i]) : 0};
     if (!rt.qual) rt.qualLen = 0;
     if (hd.status == ST_MAPPED) {
@@ -116,7 +116,7 @@ int hc_sa(void *p, int strand, uint32_t *out) {
   return 0;
 }
 
-// Align with the kernel logic on the CPU; output SAM text (malloc'd).  stats[i*4..] = fm, quick, blocks, states
+// Align with the kernel logic on the CPU; output SAM text (malloc'd).  stats[i*4..] = fm, quick, max heap, states
 int hc_align(void *p, float k, int reportType, int numSplit, uint32_t n, const char *const *names, const char *const *seqs,
              const char *const *quals, char **out, uint64_t *outLen, int32_t *stats) {
   auto *x = (HC *)p;
