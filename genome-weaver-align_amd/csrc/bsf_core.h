@@ -52,11 +52,13 @@ GWA_HD T pinv(T x) {
 #define GWA_PC(w, l)
 #endif
 
-// LDS-typed pointer on the device (plain pointer on host builds)
+// LDS-typed pointers on the device (plain pointers on host builds)
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) const uint64_t lds_cu64;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
 #else
 typedef const uint64_t lds_cu64;
+typedef uint64_t lds_u64;
 #endif
 
 template <class T, int N>
@@ -345,11 +347,21 @@ struct BsfLane {
   }
 
   // ---- QueryMask (A/QueryMask.java:41-97), computed on the fly ----
-  // The read (after replaceN_withA) is kept 2-bit packed in registers for both strands:
-  // qw[s][w] holds positions 32w..32w+31.  A 64-bit pattern window is a funnel shift of three
-  // words, a 2-bit compare and an even-bit compress (no per-read mask arrays in memory).
-  uint64_t qw[2][QW];
+  // The read (after replaceN_withA) is kept 2-bit packed for both strands: word (s, w) holds
+  // positions 32w..32w+31 of strand s.  A 64-bit pattern window is a funnel shift of three words,
+  // a 2-bit compare and an even-bit compress (no per-read mask arrays).  On the device the words
+  // live in LDS, interleaved across the workgroup (word e of thread t at qwL[e * qwS], qwS = 256):
+  // a runtime word index is then one ds_read instead of a select chain over registers.
+  lds_u64 *qwL = nullptr;
+  int qwS = 1;
+#if !defined(__HIP_DEVICE_COMPILE__)
+  uint64_t qwH[2 * QW];
+  GWA_HD void hostWords() { qwL = qwH; qwS = 1; }
+#endif
   GWA_HD void buildMasks() {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    hostWords();
+#endif
     // (the inner loop stays rolled: fully unrolled, its byte loads would all be in flight at once)
 #pragma unroll
     for (int w = 0; w < QW; ++w) {
@@ -362,17 +374,12 @@ struct BsfLane {
         v0 |= c0 << (2 * j);
         v1 |= c1 << (2 * j);
       }
-      qw[0][w] = v0;
-      qw[1][w] = v1;
+      qwL[(size_t)w * qwS] = v0;
+      qwL[(size_t)(QW + w) * qwS] = v1;
     }
   }
   GWA_HD uint64_t qword(int strand, int w) const {
-    uint64_t v = 0;
-#pragma unroll
-    for (int i = 0; i < QW; ++i) v = (strand * QW + w == i) ? qw[0][i] : v;
-#pragma unroll
-    for (int i = 0; i < QW; ++i) v = (strand * QW + w == QW + i) ? qw[1][i] : v;
-    return v;
+    return (unsigned)w < (unsigned)QW ? (uint64_t)qwL[(size_t)(strand * QW + w) * qwS] : 0ULL;
   }
   GWA_HD static uint64_t compressEven(uint64_t x) {
     x &= 0x5555555555555555ULL;
@@ -597,7 +604,9 @@ struct BsfLane {
   // on memory once per 8 (offer) or 2 (poll) levels instead of once per level.
   GWA_HD void queueAddKeyed(uint64_t e) {
     if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
+#ifdef GWA_HEAP_STATS
     maxHeap = heapSize + 1 > maxHeap ? heapSize + 1 : maxHeap;
+#endif
     const int kk = heapSize++;
     const uint64_t ek = e >> 16;
     constexpr int MAXD = 8;
@@ -1471,6 +1480,7 @@ struct BsfLane {
       GWA_PT(te);
       // children (:386-410): nextBase first -- a state from it ends the iteration -- then every
       // base still unchecked.  One loop, so the expansion is inlined once.
+#pragma unroll 1
       for (int t = -1; t < 4; ++t) {
         const int ch = t < 0 ? nextBase : t;
         if (C.state & (1 << ch)) continue;  // isChecked
@@ -1508,8 +1518,12 @@ struct BsfLane {
   int cacheIdx = -1;
   DState<R> cache;
   GWA_HD void loadState(int idx, DState<R> &d) {
+#ifdef GWA_NO_CACHE
+    d = L.arena()[idx];
+#else
     if (idx == cacheIdx) d = cache;
     else d = L.arena()[idx];
+#endif
   }
   GWA_HD void storeStateWord(int idx, int32_t w) {
     L.arena()[idx].state = w;
@@ -1564,8 +1578,10 @@ struct BsfLane {
 #pragma unroll
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
     L.arena()[id] = d;
+#ifndef GWA_NO_CACHE
     cache = d;
     cacheIdx = id;
+#endif
     (void)c;
     return id;
   }

@@ -104,6 +104,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
         BsfLane<R, QW> lane(ix, cfg, st, L, caps);
         lane.chrRank = chrRank;
         if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
+        __shared__ uint64_t qwLds1[2 * QW * 256];
+        lane.qwL = (lds_u64 *)(qwLds1 + threadIdx.x);
+        lane.qwS = 256;
         if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
         lane.initRead(reads.codes + o, m);
         lane.searchPhase(sres[r]);
@@ -119,6 +122,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   BsfLane<R, QW> lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
   if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
+  __shared__ uint64_t qwLds[2 * QW * 256];  // the lanes' 2-bit read words (BsfLane::qword)
+  lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
+  lane.qwS = 256;
   // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
   // the wavefront runs the parked reports (DP verification + traceback) together once they are at
   // least half of its live lanes, instead of once per lane on a divergent path.

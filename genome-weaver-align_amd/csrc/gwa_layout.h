@@ -80,7 +80,7 @@ struct StairTables {
   uint32_t ldsBase, ldsCount;  // that table: tab[ldsBase, ldsBase + ldsCount)
 };
 constexpr int kStairLdsWords = 2048;  // 16 KiB of LDS per workgroup
-constexpr int kLdsHeap = 16;          // first-tier priority-queue capacity (entries, in LDS)
+constexpr int kLdsHeap = 8;           // first-tier priority-queue capacity (entries, in LDS)
 
 // ---- per-read output ----
 enum : int32_t {
