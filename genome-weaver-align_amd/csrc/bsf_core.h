@@ -134,6 +134,23 @@ GWA_HD uint64_t rankOne(const Block &B, uint64_t i, int ch) {
   }
 }
 
+// One entry of the k-mer interval table (IndexView::kmer): K backward-search steps
+// (A/FMIndexOnOccTable.java:47-51) from [0, N) over `key`, first base in the high bits.
+GWA_HD uint64_t kmerInterval(const OccBlock *occ, const uint64_t C[5], uint64_t N, uint32_t key, int K) {
+  uint64_t lb = 0, ub = N;
+  for (int j = 0; j < K; ++j) {
+    const int ch = (int)((key >> (2 * (K - 1 - j))) & 3);
+    Block B0, B1;
+    loadBlock(occ, lb >> 7, B0);
+    loadBlock(occ, ub >> 7, B1);
+    const uint64_t nlb = C[ch] + rankOne(B0, lb, ch), nub = C[ch] + rankOne(B1, ub, ch);
+    if (nlb >= nub) return 0;
+    lb = nlb;
+    ub = nub;
+  }
+  return (ub << 32) | lb;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Per-lane search state (SearchState, S/BidirectionalSuffixFilter.java:658-877)
 // ---------------------------------------------------------------------------------------------
@@ -284,7 +301,7 @@ struct BsfLane {
   int nStates, heapSize, nHits, listSize, nCigar;
   int status;  // ST_*
   // instrumentation
-  int quickSteps, blocks, saReads, maxHeap;
+  int quickSteps, blocks, saReads, maxHeap, kmerLookups;
   // debug trace (nullptr in production launches): 4 words per event
   uint32_t *trace = nullptr;
   int traceCap = 0, traceN = 0;
@@ -710,7 +727,23 @@ struct BsfLane {
     int have = 0;
     int lmS = 0, lmE = 0;
     int i = 0;
+    const int K = ix.kmerK;
     for (; i < m; ++i) {
+      // at a restart from [0, N) (mark == i), the k-mer table answers the next K steps at once
+      // when none of them is empty; otherwise the steps below run one by one
+      if (K > 0 && i == mark && i + K <= m) {
+        uint32_t key = 0;
+        for (int j = 0; j < K; ++j) key = (key << 2) | (uint32_t)q(strand, i + j);
+        const uint64_t e = ix.kmer[fm][key];
+        ++kmerLookups;
+        if (e != 0) {
+          lb = e & 0xFFFFFFFFULL;
+          ub = e >> 32;
+          quickSteps += K;
+          i += K - 1;
+          continue;
+        }
+      }
       int ch = q(strand, i);
       // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
       // one 64-B block when lb and ub share a 128-position window
@@ -1379,6 +1412,7 @@ struct BsfLane {
   GWA_HD void finishQuick(OutHeader *oh) {
     oh->quickSteps = quickSteps;
     oh->blocks = blocks;
+    oh->kmerLookups = kmerLookups;
   }
   // reportExactMatchAlignment (:490-494) + FMIndexOnGenome.toGenomeCoordinate (:258-269):
   // the single exact ReadHit is the reported BESTHIT/ALLHITS/TOPL result.
@@ -1607,7 +1641,7 @@ struct BsfLane {
       stairInLds = (stairLds != nullptr && m == st.ldsM) ? 1 : 0;
       stairTab = st.tab + (stairBad ? 0 : b);
     }
-    quickSteps = blocks = saReads = maxHeap = 0;
+    quickSteps = blocks = saReads = maxHeap = kmerLookups = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains
   GWA_HD void writeSearchOutput(OutHeader *oh, OutHit *oHits, uint16_t *oCig, int outHitCap, int outCigCap) {

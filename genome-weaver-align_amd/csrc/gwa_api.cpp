@@ -65,6 +65,7 @@ struct gwa_index {
   OccBlock *d_occ[2] = {nullptr, nullptr};
   uint32_t *d_sa[2] = {nullptr, nullptr};
   uint64_t *d_text2 = nullptr, *d_textN = nullptr;
+  uint64_t *d_kmer[2] = {nullptr, nullptr};
   int64_t *d_contig = nullptr;
   int32_t *d_chrRank = nullptr;
   size_t bytes = 0;
@@ -113,6 +114,8 @@ static void freeIndexDev(gwa_index *ix) {
     if (ix->d_sa[s]) (void)hipFree(ix->d_sa[s]);
   }
   if (ix->d_text2) (void)hipFree(ix->d_text2);
+  for (int f = 0; f < 2; ++f)
+    if (ix->d_kmer[f]) (void)hipFree(ix->d_kmer[f]);
   if (ix->d_textN) (void)hipFree(ix->d_textN);
   if (ix->d_contig) (void)hipFree(ix->d_contig);
   if (ix->d_chrRank) (void)hipFree(ix->d_chrRank);
@@ -179,6 +182,18 @@ static void finishAndUpload(gwa_index *ix) {
   v.nContig = (int32_t)h.names.size();
   v.N = N;
   for (int c = 0; c < 5; ++c) v.C[c] = h.C[c];
+  // k-mer interval tables for FMQuickScan restarts (IndexView::kmer)
+  v.kmerK = kmerKFor(N);
+  if (v.kmerK > 0) {
+    const uint64_t nk = 1ULL << (2 * v.kmerK);
+    for (int f = 0; f < 2; ++f) {
+      ix->d_kmer[f] = devAlloc<uint64_t>(nk, &ix->bytes);
+      v.kmer[f] = ix->d_kmer[f];
+      buildKmerTable(v, f, v.kmerK, ix->d_kmer[f], s);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+  }
   std::vector<uint8_t>().swap(h.T);  // the text lives in HBM from here on
 }
 
@@ -523,7 +538,7 @@ static int fetch(gwa_batch *b) {
   HIPCHK(hipMemcpyAsync(b->cig.data(), b->d_cig, b->cig.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   gwa_batch_stats_t &st = b->stats;
-  st.fm_searches = st.quick_steps = st.blocks = st.states = st.quick_blocks = st.sa_reads = 0;
+  st.fm_searches = st.quick_steps = st.blocks = st.states = st.quick_blocks = st.sa_reads = st.kmer_lookups = 0;
   st.n_mapped = st.n_unmapped = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const OutHeader &h = b->oh[i];
@@ -531,6 +546,7 @@ static int fetch(gwa_batch *b) {
     st.quick_steps += (uint64_t)h.quickSteps;
     st.blocks += (uint64_t)h.blocks + (uint64_t)h.searchBlocks;
     st.quick_blocks += (uint64_t)h.blocks;
+    st.kmer_lookups += (uint64_t)h.kmerLookups;
     st.sa_reads += (uint64_t)h.saReads;
     st.states += (uint64_t)h.states;
     if (h.status == ST_MAPPED) st.n_mapped++;

@@ -180,6 +180,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 #endif
 }
 
+// one thread per k-mer (IndexView::kmer)
+__global__ void __launch_bounds__(256) kmer_table_kernel(const OccBlock *occ, IndexView ix, int K, uint64_t *out) {
+  const uint64_t key = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (key >> (2 * K)) return;
+  out[key] = kmerInterval(occ, ix.C, ix.N, (uint32_t)key, K);
+}
+
+void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream_t s) {
+  const uint64_t n = 1ULL << (2 * K);
+  hipLaunchKernelGGL(kmer_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ix.occ[fm], ix, K, out);
+}
+
 void launchQuickscan(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
                      OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace, int traceRead) {

@@ -43,10 +43,23 @@ struct IndexView {
   const uint64_t *textN;   // T, N bitmap, 64 per word
   const int64_t *contigOff;
   int32_t nContig;
-  int32_t pad;
+  int32_t kmerK;           // k of the k-mer interval tables (0 = none)
   uint64_t N;
   uint64_t C[5];  // CharacterCount.C (A/CharacterCount.java:41-50); identical for both strands
+  // Per index: the suffix interval reached by kmerK backward-search steps from [0, N) over each
+  // k-mer (first-processed base in the high bits), packed ub << 32 | lb; 0 = a step was empty.
+  // FMQuickScan restarts from [0, N) (S/FMQuickScan.java:80-89), so one lookup replaces its next
+  // kmerK steps whenever the k-mer occurs.
+  const uint64_t *kmer[2];
 };
+
+// k of the k-mer tables for a text of n bases: about log4(n) - 1, in [6, 14] (0 below 4^7)
+inline int kmerKFor(uint64_t n) {
+  int l = 0;
+  while (l < 31 && (1ULL << (2 * (l + 1))) <= n) ++l;  // l = floor(log4 n)
+  const int k = l - 1;
+  return k < 6 ? 0 : k > 14 ? 14 : k;
+}
 
 // AlignmentConfig + AlignmentScoreConfig fields read on the BSF path
 // (S/BidirectionalSuffixFilter.java:250,461,539,785; A/AlignmentScoreConfig.java:37-77)
@@ -112,7 +125,7 @@ struct OutHeader {
   int32_t chainHead[4];
   // instrumentation: FM steps, quick-scan steps, rank block loads
   int32_t fmSearches, quickSteps, blocks, states;
-  int32_t searchBlocks, saReads, maxHeap, pad1;  // maxHeap: heap high-water mark (instrumentation)
+  int32_t searchBlocks, saReads, maxHeap, kmerLookups;  // maxHeap: heap high-water mark (instrumentation)
 };
 
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at

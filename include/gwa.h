@@ -68,6 +68,7 @@ typedef struct {
   uint64_t sa_reads;       /* 4-B suffix-array gathers (exact hits + verifications) */
   uint32_t tier_reads[4];  /* reads processed per capacity tier */
   uint32_t n_mapped, n_unmapped;
+  uint64_t kmer_lookups;   /* 8-B k-mer interval-table reads by fm_quickscan */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);

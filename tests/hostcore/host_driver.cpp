@@ -17,6 +17,7 @@ using namespace gwa;
 struct HC {
   HostIndex h;
   IndexView v{};
+  std::vector<uint64_t> kmer[2];
 };
 
 // the GPU's capacity tiers (gwa_api.cpp kTiers) replayed on the CPU
@@ -97,6 +98,17 @@ void *hc_index_codes(const uint8_t *codes, uint64_t n, int32_t nc, const char *c
   v.nContig = (int32_t)x->h.names.size();
   v.N = n;
   for (int c = 0; c < 5; ++c) v.C[c] = x->h.C[c];
+  // the k-mer tables, as gwa_api.cpp builds them on the GPU (GWA_KMER_K overrides k for tests)
+  v.kmerK = getenv("GWA_KMER_K") ? atoi(getenv("GWA_KMER_K")) : kmerKFor(n);
+  if (v.kmerK > 0) {
+    const uint64_t nk = 1ULL << (2 * v.kmerK);
+    for (int f = 0; f < 2; ++f) {
+      x->kmer[f].resize(nk);
+#pragma omp parallel for schedule(static)
+      for (int64_t key = 0; key < (int64_t)nk; ++key) x->kmer[f][key] = kmerInterval(v.occ[f], v.C, n, (uint32_t)key, v.kmerK);
+      v.kmer[f] = x->kmer[f].data();
+    }
+  }
   return x;
 }
 
