@@ -1471,12 +1471,21 @@ struct BsfLane {
     upperSearches = m * 20;
     return true;
   }
+  // One call = one micro-step of the loop of align_internal (:343-477).  A poll is followed by at
+  // most ONE child expansion (an FM step); the remaining children of the same poll and the split /
+  // clip children come in later calls (xMode 1 / 2), so every lane of a wavefront performs about
+  // one FM step per call instead of the wavefront looping until its slowest lane has tried all
+  // four bases.  Nothing else touches a lane between its micro-steps, so the order of operations
+  // on its heap and arena is exactly the reference's.
+  // (the expanded state xC is re-read from the arena / cache at each micro-step rather than kept
+  // in the lane object: its flag word is always stored, so the arena copy is current)
+  int xMode = 0, xT = 0, xBase = 0, xC = 0, xNm = 0, xNextBase = 0;
   GWA_HD int searchStep() {
-    {
+    DState<R> xCS;
+    if (xMode == 0) {
       GWA_PC(PR_NSW, PR_NSL);
       if (!(heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR)) return SS_DONE;
       if (numFMIndexSearches > upperSearches) return SS_DONE;
-      GWA_PT(tl);
       GWA_PT(tp);
       const int base = queuePoll();
       // the polled state and its split chain are read once into registers
@@ -1486,65 +1495,79 @@ struct BsfLane {
       // upperBoundOfScore of the polled chain (:380), taken before the walk (which only reads)
       const int ubScore = C.nextSplit < 0 ? stateScore(C, 0, true) : chainScore(base, true);
       int c = base;
-      GWA_PA(PR_POLL, tp);
-      {
-        GWA_PT(trp);
-        // skip finished members (hasHit | isClipped | done); a chain with none left is reported
-        // (single-exit loop: no break / loop-carried flag, see quickScan)
-        while (((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) && C.nextSplit >= 0) {
-          c = C.nextSplit;
-          loadState(c, C);
-        }
-        GWA_PA(PR_REPORT, trp);
-        if ((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) {
-          pendingBase = base;
-          GWA_PA(PR_LOOP, tl);
-          return SS_REPORT;
-        }
+      // skip finished members (hasHit | isClipped | done); a chain with none left is reported
+      // (single-exit loop: no break / loop-carried flag, see quickScan)
+      while (((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) && C.nextSplit >= 0) {
+        c = C.nextSplit;
+        loadState(c, C);
       }
-      GWA_PT(tb);
+      GWA_PA(PR_POLL, tp);
+      if ((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) {
+        pendingBase = base;
+        return SS_REPORT;
+      }
       if ((C.state & 0x1F) == 0x1F) return SS_CONTINUE;  // isFinished
       const int nm = (int)(((uint32_t)C.state >> 8) & 0xFF);
       if (nm > minMismatches) return SS_CONTINUE;
       if (minMismatches - nm < 0) return SS_CONTINUE;
       if (ubScore < 0 || ubScore < bestScore) return SS_CONTINUE;
-      const int strand = cStrand(C);
-      const int nextBase = qcode(strand, cNextIdx(C));
-      GWA_PA(PR_BOUND, tb);
-      GWA_PT(te);
+      xBase = base;
+      xC = c;
+      xCS = C;
+      xNm = nm;
+      xNextBase = qcode(cStrand(C), cNextIdx(C));
+      xT = -1;
+      xMode = 1;
+    } else {
+      loadState(xC, xCS);
+    }
+    if (xMode == 1) {
       // children (:386-410): nextBase first -- a state from it ends the iteration -- then every
-      // base still unchecked.  One loop, so the expansion is inlined once.
-#pragma unroll 1
-      for (int t = -1; t < 4; ++t) {
-        const int ch = t < 0 ? nextBase : t;
-        if (C.state & (1 << ch)) continue;  // isChecked
-        C.state |= 1 << ch;                 // updateFlag
-        storeStateWord(c, C.state);
-        if (siIsEmpty(C, ch)) continue;
-        const int ns = nextStateLocal(c, C, ch);
+      // base still unchecked; one FM step per call
+      GWA_PT(te);
+      int ch = -1, tt = xT;
+      for (; tt < 4 && ch < 0; ++tt) {
+        const int cand = tt < 0 ? xNextBase : tt;
+        if (xCS.state & (1 << cand)) continue;  // isChecked
+        xCS.state |= 1 << cand;                 // updateFlag
+        if (siIsEmpty(xCS, cand)) { storeStateWord(xC, xCS.state); continue; }
+        ch = cand;
+      }
+      const int first = (xT < 0 && tt == 0) ? 1 : 0;  // the child taken is nextBase
+      xT = tt;
+      if (ch >= 0) {
+        storeStateWord(xC, xCS.state);
+        const int ns = nextStateLocal(xC, xCS, ch);
         if (ns == -2) return SS_DONE;
         if (ns >= 0) {
-          queueAdd(update(base, c, ns));
-          if (t < 0) { GWA_PA(PR_EXP1, te); GWA_PA(PR_LOOP, tl); return SS_CONTINUE; }
-        }
-      }
-      GWA_PA(PR_EXPN, te);
-      GWA_PT(ts);
-      C.state |= 1 << 4;  // updateSplitFlag
-      storeStateWord(c, C.state);
-      if (numSplit(base) < cfg.numSplit && nm + 1 <= minMismatches) {
-        const int index = cNextIdx(C);
-        if (index > cfg.indelEndSkip && m - index >= cfg.indelEndSkip) {
-          for (int clip = 0; clip < 2; ++clip) {  // split, then clip (:414-425)
-            const int ns = nextStateAfterSplit(c, clip != 0);
-            if (ns == -2) return SS_DONE;
-            if (ns >= 0) queueAdd(update(base, c, ns));
+          queueAdd(update(xBase, xC, ns));
+          if (first) {
+            xMode = 0;
+            GWA_PA(PR_EXP1, te);
+            return SS_CONTINUE;
           }
         }
+        GWA_PA(PR_EXPN, te);
+        if (xT < 4) return SS_CONTINUE;  // more candidates: next call
       }
-      GWA_PA(PR_SPLIT, ts);
-      GWA_PA(PR_LOOP, tl);
+      xMode = 2;
     }
+    // split / clip children (:412-475)
+    GWA_PT(ts);
+    xMode = 0;
+    xCS.state |= 1 << 4;  // updateSplitFlag
+    storeStateWord(xC, xCS.state);
+    if (numSplit(xBase) < cfg.numSplit && xNm + 1 <= minMismatches) {
+      const int index = cNextIdx(xCS);
+      if (index > cfg.indelEndSkip && m - index >= cfg.indelEndSkip) {
+        for (int clip = 0; clip < 2; ++clip) {  // split, then clip (:414-425)
+          const int ns = nextStateAfterSplit(xC, clip != 0);
+          if (ns == -2) return SS_DONE;
+          if (ns >= 0) queueAdd(update(xBase, xC, ns));
+        }
+      }
+    }
+    GWA_PA(PR_SPLIT, ts);
     return SS_CONTINUE;
   }
 
@@ -1631,6 +1654,7 @@ struct BsfLane {
     numFMIndexSearches = 0;
     nStates = heapSize = nHits = listSize = nCigar = 0;
     cacheIdx = -1;
+    xMode = 0;
     status = ST_UNMAPPED;
     stairBad = 0;
     stairInLds = 0;
