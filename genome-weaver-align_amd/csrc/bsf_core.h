@@ -583,20 +583,20 @@ struct BsfLane {
 
   // SearchState.score / upperBoundOfScore (:781-801), iterative over the split chain
   GWA_HD int chainScore(int s, bool upper) {
-    int len = 0;
-    for (int t = s; t >= 0; t = S(t).nextSplit) ++len;
-    int sum = 0, i = 0;
-    for (int t = s; t >= 0; t = S(t).nextSplit, ++i) {
-      int ns = len - 1 - i;
-      int nm = minK(t) - ns;
-      int mm = cProcessed(S(t)) + (upper ? cRemaining(S(t)) : 0) - nm;
-      sum += mm * cfg.matchScore - nm * cfg.mismatchPenalty - ns * cfg.splitOpenPenalty;
+    // sum over members i of mm_i*M - nm_i*N - ns_i*S with ns_i = len-1-i, nm_i = minK_i - ns_i,
+    // mm_i = processed_i (+ remaining_i) - nm_i, regrouped so one walk of the chain suffices
+    int len = 0, sumPR = 0, sumK = 0;
+    for (int t = s; t >= 0;) {
+      const DState<R> &x = S(t);
+      sumPR += cProcessed(x) + (upper ? cRemaining(x) : 0);
+      sumK += (int)(((uint32_t)x.state >> 8) & 0xFF);
+      ++len;
+      t = x.nextSplit;
     }
-    return sum;
+    const int T = len * (len - 1) / 2;
+    const int M = cfg.matchScore;
+    return M * sumPR - (M + cfg.mismatchPenalty) * (sumK - T) - cfg.splitOpenPenalty * T;
   }
-  // StateQueue comparator (:141-150) as a cached sortable key: priority asc, score() desc,
-  // processed bases desc.  Keys are live in the reference; the only mutations that change them
-  // (SearchState.update splicing a chain, setLowerBoundOfK) call refreshKeys().
   GWA_HD uint64_t keyOf(int s) {
     if (s == cacheIdx && cache.nextSplit < 0) {
       const int sc0 = stateScore(cache, 0, false);
@@ -961,8 +961,10 @@ struct BsfLane {
           const int ns = dpBlock(x, carry, vp[r], vn[r]);
           D[r] += ns;
           carry = ns;
+#ifndef GWA_EXP_NOSTORE
           hvp[((size_t)(j + 1) * bMax + r) * is] = vp[r];
           hvn[((size_t)(j + 1) * bMax + r) * is] = vn[r];
+#endif
           wmask |= 1u << r;
         }
       }
@@ -988,7 +990,9 @@ struct BsfLane {
       } else {
         while (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
       }
+#ifndef GWA_EXP_NOSTORE
       wr[(size_t)j * is] = (uint8_t)pend;
+#endif
       pend = wmask;
       if (bCeil == bMax) {
         const int dl = pick(D, bCeil - 1);
@@ -1303,12 +1307,11 @@ struct BsfLane {
   }
 
   // nextStateAfterSplit / nextStateAfterClipping (:803-838); -1 null, -2 overflow
-  GWA_HD int nextStateAfterSplit(int c, bool clip) {
-    invalidateCache();
-    updateSplitFlag(c);
-    const int mk = minK(c);
+  GWA_HD int nextStateAfterSplit(const DState<R> &cs, bool clip, uint64_t *key) {
+    // cs = register copy of the expanded state, its split flag already stored by the caller
+    const int mk = (int)(((uint32_t)cs.state >> 8) & 0xFF);
     if (!(mk < k)) return -1;
-    const DState<R> cs = S(c);
+    const int pr = (int)(((uint32_t)cs.state >> 16) & 0xFF);
     // Cursor.split (S/Cursor.java:130-156)
     int strand = cStrand(cs), dir = cDir(cs);
     int ld, ls, le, lc, lp, rdr, rs, re, rc, rp;
@@ -1327,46 +1330,49 @@ struct BsfLane {
         rdr = dir; rs = cs.cursor; re = cs.end; rc = cs.cursor; rp = cs.cursor;
       }
     }
-    int a = allocState();
+    const int a = allocState();
     if (a < 0) return -2;
+    const int b = allocState();
+    if (b < 0) return -2;
+    DState<R> d = cs;  // currentSi, siTable carried over
+    setCursor(d, strand, ld, ls, le, lc, lp);
     {
-      DState<R> d = cs;  // currentSi, siTable carried over
-      setCursor(d, strand, ld, ls, le, lc, lp);
       // ReadAlignmentNFA.nextStateAfterSplit (S/ReadAlignmentNFA.java:107-114)
       int height = cs.nrows - 1;
       d.nrows = (uint8_t)(height < 0 ? 0 : height);
       d.kOffset = (uint8_t)(cs.kOffset + 1);
       for (int i = 0; i < R; ++i) d.nfa[i] = i < height ? (uint64_t)jshl(1, height + i - 1) : 0;
-      d.state = packState(curACGT(c), mk, prio(c), hasHit(c));
-      d.nextSplit = -1;
-      S(a) = d;
+      const int cur = ((uint32_t)cs.state >> 5) & 7;
+      d.state = packState(cur > 4 ? 4 : cur, mk, pr, (((uint32_t)cs.state >> 24) & 1) != 0);
+      d.nextSplit = b;
     }
-    int b = allocState();
-    if (b < 0) return -2;
-    {
-      DState<R> t;
-      t.meta = 0;
-      setCursor(t, strand, rdr, rs, re, rc, rp);
-      t.curLb = t.curUb = 0;
-      t.nextSplit = -1;
-      t.state = packState(4, mk, prio(c), false);
-      if (!clip) {
-        siInit(t, rdr);
-        t.meta |= M_NFAVALID;
-        t.nrows = (uint8_t)(k + 1);
-        t.kOffset = 0;
-        for (int i = 0; i < R; ++i) t.nfa[i] = i <= k ? (uint64_t)jshl(1, k + i) : 0;
-      } else {
-        for (int i = 0; i < 4; ++i) t.lb[i] = t.ub[i] = 0;
-        t.bBase = 0;
-        t.nrows = 0;
-        t.kOffset = 0;
-        for (int i = 0; i < R; ++i) t.nfa[i] = 0;
-        t.state |= 1 << 25;  // updateClippedFlag
-      }
-      S(b) = t;
+    DState<R> t;
+    t.meta = 0;
+    setCursor(t, strand, rdr, rs, re, rc, rp);
+    t.curLb = t.curUb = 0;
+    t.nextSplit = -1;
+    t.state = packState(4, mk, pr, false);
+    if (!clip) {
+      siInit(t, rdr);
+      t.meta |= M_NFAVALID;
+      t.nrows = (uint8_t)(k + 1);
+      t.kOffset = 0;
+      for (int i = 0; i < R; ++i) t.nfa[i] = i <= k ? (uint64_t)jshl(1, k + i) : 0;
+    } else {
+      for (int i = 0; i < 4; ++i) t.lb[i] = t.ub[i] = 0;
+      t.bBase = 0;
+      t.nrows = 0;
+      t.kOffset = 0;
+      for (int i = 0; i < R; ++i) t.nfa[i] = 0;
+      t.state |= 1 << 25;  // updateClippedFlag
     }
-    S(a).nextSplit = b;
+    S(a) = d;
+    S(b) = t;
+    // keyOf(a) for the chain [a -> b] from the registers (chainScore with one split)
+    const int M = cfg.matchScore;
+    const int sc = M * (cProcessed(d) + cProcessed(t)) - (M + cfg.mismatchPenalty) * (2 * mk - 1) - cfg.splitOpenPenalty;
+    *key = ((uint64_t)pr << 40) | ((uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc) & 0xFFFFFFFFULL) << 8 |
+           (uint64_t)(255 - cProcessed(d));
     return a;
   }
 
@@ -1557,13 +1563,18 @@ struct BsfLane {
     xMode = 0;
     xCS.state |= 1 << 4;  // updateSplitFlag
     storeStateWord(xC, xCS.state);
-    if (numSplit(xBase) < cfg.numSplit && xNm + 1 <= minMismatches) {
+    const int nsplit = (xC == xBase && xCS.nextSplit < 0) ? 0 : numSplit(xBase);
+    if (nsplit < cfg.numSplit && xNm + 1 <= minMismatches) {
       const int index = cNextIdx(xCS);
       if (index > cfg.indelEndSkip && m - index >= cfg.indelEndSkip) {
         for (int clip = 0; clip < 2; ++clip) {  // split, then clip (:414-425)
-          const int ns = nextStateAfterSplit(xC, clip != 0);
+          uint64_t key = 0;
+          const int ns = nextStateAfterSplit(xCS, clip != 0, &key);
           if (ns == -2) return SS_DONE;
-          if (ns >= 0) queueAdd(update(xBase, xC, ns));
+          if (ns >= 0) {
+            if (xC == xBase) queueAddKeyed((key << 16) | (uint64_t)ns);  // update(base, base, ns) == ns
+            else queueAdd(update(xBase, xC, ns));
+          }
         }
       }
     }
