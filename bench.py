@@ -160,11 +160,14 @@ def main():
                          "BSF path (oracle/), same index" % ns}
         log("cpu baseline: %.0f reads/s (%d reads in %.1fs)" % (ns / ct, ns, ct))
 
-    # roofline of the dominant kernel: algorithmic bytes = 64 B per Occ block read (+4 B per SA gather)
+    # roofline of the dominant kernel.  Algorithmic bytes: 64 B per distinct
+    # Occ block of every reference FM step (+4 B per SA gather).  Quick-scan steps that this kernel answers
+    # without Occ blocks (k-mer table, single-row text compare) are counted at the §8d lower bound of one
+    # block per step.
     steps = args.steps
     q_ms, s_ms = qms / steps, sms / steps
-    q_bytes = 64.0 * st.quick_blocks
-    s_bytes = 64.0 * (st.blocks - st.quick_blocks) + 4.0 * st.sa_reads
+    q_bytes = 64.0 * (st.quick_blocks + st.quick_short_steps) + 4.0 * st.quick_sa_reads
+    s_bytes = 64.0 * (st.blocks - st.quick_blocks) + 4.0 * (st.sa_reads - st.quick_sa_reads)
     if q_ms >= s_ms:
         dom, ach_bytes, dom_ms = "fm_quickscan", q_bytes, q_ms
     else:
@@ -188,6 +191,12 @@ def main():
                    "fm_searches_per_read": st.fm_searches / reads_per_step,
                    "quick_steps_per_read": st.quick_steps / reads_per_step,
                    "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
+                   "quick_short_steps_per_read": st.quick_short_steps / reads_per_step,
+                   "rank_kernel": {"kernel": "fm_quickscan", "algorithmic_bytes_per_launch": q_bytes,
+                                   "avg_launch_ms": q_ms,
+                                   "achieved_GBs": q_bytes / (q_ms * 1e-3) / 1e9 if q_ms > 0 else 0.0,
+                                   "frac": (q_bytes / (q_ms * 1e-3) / 1e9 if q_ms > 0 else 0.0) / HBM_PEAK_GBS,
+                                   "traffic": _pmc_traffic("fm_quickscan", workload)[0]},
                    "mapped": st.n_mapped, "unmapped": st.n_unmapped, "index_build_s": t_index,
                    "index_gb": gi.deviceBytes() / 1e9, "parity": parity},
     }

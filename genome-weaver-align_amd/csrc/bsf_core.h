@@ -10,6 +10,7 @@
 // the kernel logic only, by g++ in tests/ (never a product fallback: the C-ABI requires a GPU).
 #pragma once
 #include <math.h>
+#include <string.h>
 
 #include "gwa_layout.h"
 
@@ -135,11 +136,12 @@ GWA_HD uint64_t rankOne(const Block &B, uint64_t i, int ch) {
 }
 
 // One entry of the k-mer interval table (IndexView::kmer): K backward-search steps
-// (A/FMIndexOnOccTable.java:47-51) from [0, N) over `key`, first base in the high bits.
+// (A/FMIndexOnOccTable.java:47-51) from [0, N) over `key`, first-processed base in the low bits
+// (the order of the 2-bit packed read words, so a key is a shifted window of them).
 GWA_HD uint64_t kmerInterval(const OccBlock *occ, const uint64_t C[5], uint64_t N, uint32_t key, int K) {
   uint64_t lb = 0, ub = N;
   for (int j = 0; j < K; ++j) {
-    const int ch = (int)((key >> (2 * (K - 1 - j))) & 3);
+    const int ch = (int)((key >> (2 * j)) & 3);
     Block B0, B1;
     loadBlock(occ, lb >> 7, B0);
     loadBlock(occ, ub >> 7, B1);
@@ -301,7 +303,7 @@ struct BsfLane {
   int nStates, heapSize, nHits, listSize, nCigar;
   int status;  // ST_*
   // instrumentation
-  int quickSteps, blocks, saReads, maxHeap, kmerLookups;
+  int quickSteps, blocks, saReads, maxHeap, kmerLookups, shortSteps;
   // debug trace (nullptr in production launches): 4 words per event
   uint32_t *trace = nullptr;
   int traceCap = 0, traceN = 0;
@@ -319,12 +321,73 @@ struct BsfLane {
   GWA_HD BsfLane(const IndexView &ix_, const SearchConfig &c_, const StairTables &s_, LaneMem<R> L_, Caps caps_)
       : ix(ix_), cfg(c_), st(s_), L(L_), caps(caps_) {}
 
-  // q[strand][i] after replaceN_withA (S/BidirectionalSuffixFilter.java:281-291): q[1] is the
-  // complement (not the reverse complement) of q[0] (:193); N -> A on both.
+  // The read, 2-bit packed for both strands after replaceN_withA (S/BidirectionalSuffixFilter.java:
+  // 281-291): q[1] is the complement (not the reverse complement) of q[0] (:193); N -> A on both.
+  // Word w of strand s holds positions 32w..32w+31, position p at bits 2(p&31); positions >= m are 0.
+  // The codes are read 16 bytes at a time (reads start 16-B aligned in HBM, ReadsView); returns the
+  // number of N codes (fastCount(N), A/ACGTSequence.java:456-477).
+  GWA_HD static uint32_t pack4(uint32_t v) {  // 4 byte codes -> 4 two-bit fields
+    uint32_t x = v & 0x03030303u;
+    x = (x | (x >> 6)) & 0x000F000Fu;
+    return (x | (x >> 12)) & 0xFFu;
+  }
+  GWA_HD static uint32_t nbits4(uint32_t v) {  // 4 byte codes -> 4 N flags
+    uint32_t x = (v >> 2) & 0x01010101u;
+    return (x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu;
+  }
+  GWA_HD int loadWords(uint64_t (&w0)[QW], uint64_t (&w1)[QW]) const {
+    int countN = 0;
+#pragma unroll
+    for (int w = 0; w < QW; ++w) {
+      uint64_t a0 = 0, a1 = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // 16 codes per half word
+        const int p0 = 32 * w + 16 * h;
+        if (p0 < m) {
+          uint32_t v[4];
+#if defined(__HIP_DEVICE_COMPILE__)
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 c = *reinterpret_cast<const u32x4 *>(rd + p0);
+          v[0] = c.x; v[1] = c.y; v[2] = c.z; v[3] = c.w;
+#else
+          memcpy(v, rd + p0, 16);
+#endif
+          uint32_t lo = 0, nb = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            lo |= pack4(v[j]) << (8 * j);
+            nb |= nbits4(v[j]) << (4 * j);
+          }
+          const int valid = m - p0;  // positions p0 + [0, valid) belong to the read
+          const uint32_t vm = valid >= 16 ? 0xFFFFu : ((1u << valid) - 1u);
+          nb &= vm;
+          // 2-bit field mask of the valid, non-N positions
+          uint32_t keep = 0;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) keep |= (((vm & ~nb) >> j) & 1u) * (3u << (2 * j));
+          countN += popc64(nb);
+          a0 |= (uint64_t)(lo & keep) << (32 * h);
+          a1 |= (uint64_t)((lo ^ 0xFFFFFFFFu) & keep) << (32 * h);
+        }
+      }
+      w0[w] = a0;
+      w1[w] = a1;
+    }
+    return countN;
+  }
+  // quick-scan kernel: the read words in registers
+  uint64_t pw0[QW], pw1[QW];
   GWA_HD int q(int strand, int i) const {
-    int c = rd[i];
-    if (c >= 4) return 0;
-    return strand ? 3 - c : c;
+    const uint64_t x = strand ? pick(pw1, i >> 5) : pick(pw0, i >> 5);
+    return (int)((x >> (2 * (i & 31))) & 3);
+  }
+  // bits [2i, 2i + 2K) of strand `strand` (K <= 16): q(i + j) at bits 2j
+  GWA_HD uint32_t qWindow(int strand, int i, int K) const {
+    const int w = i >> 5, sh = 2 * (i & 31);
+    const uint64_t a = strand ? pick(pw1, w) : pick(pw0, w);
+    const uint64_t b = (w + 1 < QW) ? (strand ? pick(pw1, w + 1) : pick(pw0, w + 1)) : 0ULL;
+    const uint64_t x = sh ? (a >> sh) | (b << (64 - sh)) : a;
+    return (uint32_t)(x & ((1ULL << (2 * K)) - 1ULL));
   }
 
   // ---- FM index primitives (A/FMIndexOnGenome.java:121-225) ----
@@ -379,20 +442,12 @@ struct BsfLane {
 #if !defined(__HIP_DEVICE_COMPILE__)
     hostWords();
 #endif
-    // (the inner loop stays rolled: fully unrolled, its byte loads would all be in flight at once)
+    uint64_t v0[QW], v1[QW];
+    loadWords(v0, v1);
 #pragma unroll
     for (int w = 0; w < QW; ++w) {
-      uint64_t v0 = 0, v1 = 0;
-      const int n = m - w * 32 < 32 ? m - w * 32 : 32;
-#pragma unroll 1
-      for (int j = 0; j < n; ++j) {
-        const int c = rd[w * 32 + j];
-        const uint64_t c0 = c >= 4 ? 0 : c, c1 = c >= 4 ? 0 : 3 - c;  // q(0, i), q(1, i)
-        v0 |= c0 << (2 * j);
-        v1 |= c1 << (2 * j);
-      }
-      qwL[(size_t)w * qwS] = v0;
-      qwL[(size_t)(QW + w) * qwS] = v1;
+      qwL[(size_t)w * qwS] = v0[w];
+      qwL[(size_t)(QW + w) * qwS] = v1[w];
     }
   }
   GWA_HD uint64_t qword(int strand, int w) const {
@@ -716,7 +771,27 @@ struct BsfLane {
   }
 
   // ---- FMQuickScan.scanMismatchLocations (S/FMQuickScan.java:66-94) ----
-  struct Scan { uint64_t lb, ub; int numMismatches, lmStart; };
+  // uniq != 0: [lb, ub) is one row whose suffix-array value is tp (the FM steps ran in text mode)
+  struct Scan { uint64_t lb, ub, tp; int numMismatches, lmStart, uniq; };
+
+  // One reference FM step from a single-row interval, read off the text instead of the Occ blocks.
+  // For a one-row interval [l, l+1) with SA value p, backwardSearch(c) (A/FMIndexOnOccTable.java:47-51)
+  // is non-empty iff BWT[l] == c, i.e. iff the cyclic text character before rotation p is c
+  // (A/BWTransform.java:172-179), and the extended interval is again one row, with SA value p-1.
+  // fm 0 indexes T, fm 1 indexes R = reverse(T), whose character R[p-1] is T[N-p]; both are
+  // read from the 2-bit forward text (+ N bitmap), one word per 32 (64) steps.
+  struct TextWalk {
+    int64_t w2 = -1, wN = -1;
+    uint64_t c2 = 0, cN = 0;
+  };
+  GWA_HD int textBefore(int fm, uint64_t p, TextWalk &tw) {
+    const uint64_t N = ix.N;
+    const uint64_t t = fm ? (p == 0 ? 0 : N - p) : (p == 0 ? N - 1 : p - 1);
+    const int64_t a = (int64_t)(t >> 5), b = (int64_t)(t >> 6);
+    if (a != tw.w2) { tw.c2 = ix.text2[a]; tw.w2 = a; }
+    if (b != tw.wN) { tw.cN = ix.textN[b]; tw.wN = b; }
+    return ((tw.cN >> (t & 63)) & 1) ? 4 : (int)((tw.c2 >> ((t & 31) * 2)) & 3);
+  }
 
   GWA_HD Scan quickScan(int strand) {
     const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
@@ -726,36 +801,55 @@ struct BsfLane {
     // mis-lowered by the gfx950 backend in our tests); `have` is an int 0/1.
     int have = 0;
     int lmS = 0, lmE = 0;
+    // text mode (textBefore): once the interval is a single row, each further step is one text
+    // character compare; tp = SA value of that row.  uniq is an int 0/1 for the same reason as have.
+    int uniq = 0;
+    uint64_t tp = 0;
+    TextWalk tw;
     int i = 0;
     const int K = ix.kmerK;
     for (; i < m; ++i) {
       // at a restart from [0, N) (mark == i), the k-mer table answers the next K steps at once
       // when none of them is empty; otherwise the steps below run one by one
       if (K > 0 && i == mark && i + K <= m) {
-        uint32_t key = 0;
-        for (int j = 0; j < K; ++j) key = (key << 2) | (uint32_t)q(strand, i + j);
+        const uint32_t key = qWindow(strand, i, K);
         const uint64_t e = ix.kmer[fm][key];
         ++kmerLookups;
         if (e != 0) {
           lb = e & 0xFFFFFFFFULL;
           ub = e >> 32;
           quickSteps += K;
+          shortSteps += K;
           i += K - 1;
+          const int u = ub - lb == 1 ? 1 : 0;
+          if (u) { tp = ix.sa[fm][lb]; ++saReads; }
+          uniq = u;
           continue;
         }
       }
       int ch = q(strand, i);
-      // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
-      // one 64-B block when lb and ub share a 128-position window
-      Block B;
-      loadBlock(ix.occ[fm], lb >> 7, B);
-      ++blocks;
-      uint64_t nlb = ix.C[ch] + rankOne(B, lb, ch);
-      if ((ub >> 7) != (lb >> 7)) {
-        loadBlock(ix.occ[fm], ub >> 7, B);
+      uint64_t nlb, nub;
+      if (uniq) {
+        const int tc = textBefore(fm, tp, tw);
+        ++shortSteps;
+        const int hit = tc == ch ? 1 : 0;
+        nlb = lb;
+        nub = hit ? ub : lb;
+        tp = hit ? (tp == 0 ? ix.N - 1 : tp - 1) : tp;
+      } else {
+        // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
+        // one 64-B block when lb and ub share a 128-position window
+        Block B;
+        loadBlock(ix.occ[fm], lb >> 7, B);
         ++blocks;
+        nlb = ix.C[ch] + rankOne(B, lb, ch);
+        if ((ub >> 7) != (lb >> 7)) {
+          loadBlock(ix.occ[fm], ub >> 7, B);
+          ++blocks;
+        }
+        nub = ix.C[ch] + rankOne(B, ub, ch);
+        if (nub - nlb == 1) { tp = ix.sa[fm][nlb]; ++saReads; uniq = 1; }
       }
-      uint64_t nub = ix.C[ch] + rankOne(B, ub, ch);
       ++quickSteps;
       tr(16 + strand, (uint32_t)(i | (ch << 16)), (uint32_t)nlb, (uint32_t)nub);
       const int empty = nlb >= nub ? 1 : 0;
@@ -767,6 +861,7 @@ struct BsfLane {
       lb = empty ? 0 : nlb;
       ub = empty ? ix.N : nub;
       mark = empty ? i + 1 : mark;
+      uniq = empty ? 0 : uniq;
     }
     {
       const int better = (have ^ 1) | ((lmE - lmS) < (i - mark) ? 1 : 0);
@@ -774,7 +869,7 @@ struct BsfLane {
       lmE = better ? i : lmE;
     }
     Scan s;
-    s.lb = lb; s.ub = ub; s.numMismatches = nmm; s.lmStart = lmS;
+    s.lb = lb; s.ub = ub; s.tp = tp; s.numMismatches = nmm; s.lmStart = lmS; s.uniq = uniq;
     return s;
   }
 
@@ -1401,8 +1496,7 @@ struct BsfLane {
     oh->nChains = oh->nHits = oh->nCigar = 0;
     oh->status = ST_UNMAPPED;
     {
-      int countN = 0;
-      for (int i = 0; i < m; ++i) countN += rd[i] == 4;
+      const int countN = loadWords(pw0, pw1);
       if (countN > k) { finishQuick(oh); return 0; }
     }
     Scan sF = quickScan(0);
@@ -1419,13 +1513,16 @@ struct BsfLane {
     oh->quickSteps = quickSteps;
     oh->blocks = blocks;
     oh->kmerLookups = kmerLookups;
+    oh->quickSa = saReads;
+    oh->quickShort = shortSteps;
   }
   // reportExactMatchAlignment (:490-494) + FMIndexOnGenome.toGenomeCoordinate (:258-269):
   // the single exact ReadHit is the reported BESTHIT/ALLHITS/TOPL result.
   GWA_HD void reportExact(const Scan &s, int strand, OutHeader *oh, OutHit *oHits, uint16_t *oCig) {
+    int64_t sav = s.uniq ? (int64_t)s.tp : (int64_t)ix.sa[strand == 0 ? 1 : 0][s.lb];
+    if (!s.uniq) ++saReads;
     finishQuick(oh);
-    oh->saReads = 1;
-    int64_t pos = strand == 0 ? (int64_t)ix.N - (int64_t)ix.sa[1][s.lb] : (int64_t)ix.sa[0][s.lb];
+    int64_t pos = strand == 0 ? (int64_t)ix.N - sav : sav;
     if (strand == 0) pos -= m;
     pos += 1;
     int32_t chr, p;
@@ -1676,7 +1773,7 @@ struct BsfLane {
       stairInLds = (stairLds != nullptr && m == st.ldsM) ? 1 : 0;
       stairTab = st.tab + (stairBad ? 0 : b);
     }
-    quickSteps = blocks = saReads = maxHeap = kmerLookups = 0;
+    quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains
   GWA_HD void writeSearchOutput(OutHeader *oh, OutHit *oHits, uint16_t *oCig, int outHitCap, int outCigCap) {

@@ -85,11 +85,11 @@ struct gwa_batch {
   std::vector<uint64_t> nameOff, seqOff, qualOff;
   bool hasQual = false;
   std::vector<uint8_t> codes;
-  std::vector<uint32_t> codeOff;
+  std::vector<uint32_t> codeOff, codeLen;
   int maxM = 0, kmax = 0, R = 4;
   // device
   uint8_t *d_codes = nullptr;
-  uint32_t *d_off = nullptr;
+  uint32_t *d_off = nullptr, *d_len = nullptr;
   ScanRes *d_sres = nullptr;
   OutHeader *d_oh = nullptr;
   OutHit *d_hits = nullptr;
@@ -296,7 +296,7 @@ void gwa_index_close(gwa_index_t *ix) {
 void gwa_free(void *p) { free(p); }
 
 static void freeBatchDev(gwa_batch *b) {
-  void *ps[] = {b->d_codes, b->d_off, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_count,
+  void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_count,
                 b->d_stair, b->d_stairBase};
   for (void *p : ps)
     if (p) (void)hipFree(p);
@@ -330,6 +330,7 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     b->codeOff.resize(n + 1);
     std::vector<int> lens;
     std::vector<char> seen(256, 0);
+    b->codeLen.resize(n);
     for (uint32_t i = 0; i < n; ++i) {
       b->codeOff[i] = (uint32_t)b->codes.size();
       for (uint64_t p = b->seqOff[i]; p < b->seqOff[i + 1]; ++p) {
@@ -337,9 +338,12 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
         if (c != ' ') b->codes.push_back(to3bit((unsigned char)c));
       }
       int m = (int)(b->codes.size() - b->codeOff[i]);
+      b->codeLen[i] = (uint32_t)m;
+      b->codes.resize((b->codes.size() + 15) & ~(size_t)15, 0);  // 16-B aligned, zero-padded (ReadsView)
       b->maxM = std::max(b->maxM, m);
       if (m <= 255 && !seen[(size_t)m]) { seen[(size_t)m] = 1; lens.push_back(m); }
     }
+    b->codes.resize(b->codes.size() + 16, 0);
     b->codeOff[n] = (uint32_t)b->codes.size();
     // k per length (AlignmentScoreConfig.getMaximumEditDistance)
     for (int m : lens) {
@@ -354,6 +358,7 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     hipStream_t s = ix->stream;
     b->d_codes = devUpload(b->codes, s, nullptr);
     b->d_off = devUpload(b->codeOff, s, nullptr);
+    b->d_len = devUpload(b->codeLen, s, nullptr);
     b->d_stair = devUpload(tab, s, nullptr);
     b->d_stairBase = devUpload(base, s, nullptr);
     b->st.tab = b->d_stair;
@@ -406,7 +411,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     HIPCHK(hipSetDevice(ix->device));
     hipStream_t s = ix->stream;
     memset(&b->stats, 0, sizeof(b->stats));
-    ReadsView rv{b->d_codes, b->d_off, b->n};
+    ReadsView rv{b->d_codes, b->d_off, b->d_len, b->n};
     hipEvent_t e0, e1, e2;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
@@ -416,7 +421,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     const char *qtre = getenv("GWA_QTRACE_READ");
     static uint32_t *d_qtrace = nullptr;
     if (qtre && !d_qtrace) { HIPCHK(hipMalloc(&d_qtrace, 4 * 65540)); HIPCHK(hipMemset(d_qtrace, 0, 4 * 65540)); }
-    launchQuickscan(ix->view, b->scfg, rv, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, b->d_list[0],
+    launchQuickscan(b->maxM <= 128 ? 4 : 8, ix->view, b->scfg, rv, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, b->d_list[0],
                     b->d_count, s, qtre ? d_qtrace : nullptr, qtre ? atoi(qtre) : -1);
     if (qtre) {
       std::vector<uint32_t> tv(65537);
@@ -539,6 +544,7 @@ static int fetch(gwa_batch *b) {
   HIPCHK(hipStreamSynchronize(s));
   gwa_batch_stats_t &st = b->stats;
   st.fm_searches = st.quick_steps = st.blocks = st.states = st.quick_blocks = st.sa_reads = st.kmer_lookups = 0;
+  st.quick_short_steps = st.quick_sa_reads = 0;
   st.n_mapped = st.n_unmapped = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const OutHeader &h = b->oh[i];
@@ -547,7 +553,9 @@ static int fetch(gwa_batch *b) {
     st.blocks += (uint64_t)h.blocks + (uint64_t)h.searchBlocks;
     st.quick_blocks += (uint64_t)h.blocks;
     st.kmer_lookups += (uint64_t)h.kmerLookups;
-    st.sa_reads += (uint64_t)h.saReads;
+    st.sa_reads += (uint64_t)h.saReads + (uint64_t)h.quickSa;
+    st.quick_sa_reads += (uint64_t)h.quickSa;
+    st.quick_short_steps += (uint64_t)h.quickShort;
     st.states += (uint64_t)h.states;
     if (h.status == ST_MAPPED) st.n_mapped++;
     else if (h.status == ST_UNMAPPED) st.n_unmapped++;

@@ -30,6 +30,7 @@ __device__ __forceinline__ void waveAppend(bool need, uint32_t value, uint32_t *
   }
 }
 
+template <int QW>
 __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
                                                            OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
                                                            uint32_t *searchList, uint32_t *searchCount, uint32_t *trace,
@@ -38,16 +39,16 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
   bool need = false;
   if (r < reads.n) {
     const uint32_t o = reads.off[r];
-    const int m = (int)(reads.off[r + 1] - o);
+    const int m = (int)reads.len[r];
     OutHeader *h = oh + r;
-    if (m > 255) {
+    if (m > 32 * QW || m > 255) {
       h->status = ST_TOO_LONG;
       h->nChains = h->nHits = h->nCigar = 0;
     } else {
       StairTables st{};
       LaneMem<4> L{};
       Caps caps{};
-      BsfLane<4> lane(ix, cfg, st, L, caps);
+      BsfLane<4, QW> lane(ix, cfg, st, L, caps);
       if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
       lane.initRead(reads.codes + o, m);
       need = lane.quickPhase(sres + r, h, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap) != 0;
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
       if (i < n) {
         r = list[i];
         const uint32_t o = reads.off[r];
-        const int m = (int)(reads.off[r + 1] - o);
+        const int m = (int)reads.len[r];
         BsfLane<R, QW> lane(ix, cfg, st, L, caps);
         lane.chrRank = chrRank;
         if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
@@ -146,7 +147,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
         if (i < n) {
           r = list[i];
           const uint32_t o = reads.off[r];
-          const int m = (int)(reads.off[r + 1] - o);
+          const int m = (int)reads.len[r];
           lane.trace = nullptr;
           if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; lane.traceN = 0; }
           lane.initRead(reads.codes + o, m);
@@ -192,13 +193,17 @@ void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream
   hipLaunchKernelGGL(kmer_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ix.occ[fm], ix, K, out);
 }
 
-void launchQuickscan(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
+void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
                      OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace, int traceRead) {
   if (reads.n == 0) return;
   dim3 grid((reads.n + 255) / 256);
-  hipLaunchKernelGGL(fm_quickscan_kernel, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, ohits, ocig, hitCap, cigCap,
-                     searchList, searchCount, trace, traceRead);
+  if (QW == 4)
+    hipLaunchKernelGGL(fm_quickscan_kernel<4>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, ohits, ocig, hitCap, cigCap,
+                       searchList, searchCount, trace, traceRead);
+  else
+    hipLaunchKernelGGL(fm_quickscan_kernel<8>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, ohits, ocig, hitCap, cigCap,
+                       searchList, searchCount, trace, traceRead);
 }
 
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,

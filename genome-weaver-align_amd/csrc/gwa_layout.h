@@ -75,10 +75,12 @@ struct SearchConfig {
   int32_t waitQ16;
 };
 
-// Read batch as resident in HBM: 2-bit-per-byte codes (0..4) per read, concatenated.
+// Read batch as resident in HBM: one byte code (0..4) per base; every read starts at a 16-B
+// aligned offset and is zero-padded to a multiple of 16 B, so a lane loads it 16 codes at a time.
 struct ReadsView {
   const uint8_t *codes;
-  const uint32_t *off;  // n+1 offsets into codes
+  const uint32_t *off;  // n offsets into codes (multiples of 16)
+  const uint32_t *len;  // n read lengths
   uint32_t n;
 };
 
@@ -126,6 +128,8 @@ struct OutHeader {
   // instrumentation: FM steps, quick-scan steps, rank block loads
   int32_t fmSearches, quickSteps, blocks, states;
   int32_t searchBlocks, saReads, maxHeap, kmerLookups;  // maxHeap: heap high-water mark (instrumentation)
+  // quick-scan steps answered without Occ blocks (k-mer table or single-row text compare)
+  int32_t quickShort, quickSa, pad_[2];  // quickSa: SA gathers of the quick scan
 };
 
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at

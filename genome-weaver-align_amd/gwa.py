@@ -40,7 +40,8 @@ class BatchStats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("quickscan_ms", ctypes.c_double), ("search_ms", ctypes.c_double),
                 ("fm_searches", ctypes.c_uint64), ("quick_steps", ctypes.c_uint64), ("blocks", ctypes.c_uint64),
                 ("quick_blocks", ctypes.c_uint64), ("states", ctypes.c_uint64), ("sa_reads", ctypes.c_uint64), ("tier_reads", ctypes.c_uint32 * 4),
-                ("n_mapped", ctypes.c_uint32), ("n_unmapped", ctypes.c_uint32), ("kmer_lookups", ctypes.c_uint64)]
+                ("n_mapped", ctypes.c_uint32), ("n_unmapped", ctypes.c_uint32), ("kmer_lookups", ctypes.c_uint64),
+                ("quick_short_steps", ctypes.c_uint64), ("quick_sa_reads", ctypes.c_uint64)]
 
 
 _lib = None

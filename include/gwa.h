@@ -69,6 +69,8 @@ typedef struct {
   uint32_t tier_reads[4];  /* reads processed per capacity tier */
   uint32_t n_mapped, n_unmapped;
   uint64_t kmer_lookups;   /* 8-B k-mer interval-table reads by fm_quickscan */
+  uint64_t quick_short_steps; /* FMQuickScan steps answered without Occ blocks (k-mer table, single-row text compare) */
+  uint64_t quick_sa_reads; /* of sa_reads, by fm_quickscan */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);

@@ -39,6 +39,8 @@ static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int max
     std::vector<uint8_t> codes;
     for (const char *c = seqs[i]; *c; ++c)
       if (*c != ' ') codes.push_back(to3bit((unsigned char)*c));
+    const size_t mlen = codes.size();
+    codes.resize(((mlen + 15) & ~(size_t)15) + 16, 0);  // 16-B padded, as ReadsView
     OutHeader hd{};
     std::vector<uint32_t> tv(65537, 0);
     bool traced = false;
@@ -49,7 +51,7 @@ static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int max
       const char *tre = getenv("GWA_TRACE_READ");
       const char *qtre = getenv("GWA_QTRACE_READ");
       if ((tre && atoi(tre) == (int)i) || (qtre && atoi(qtre) == (int)i)) { lane.trace = tv.data() + 1; lane.traceCap = 65536; traced = true; }
-      lane.initRead(codes.data(), (int)codes.size());
+      lane.initRead(codes.data(), (int)mlen);
       ScanRes sr{};
       if (lane.quickPhase(&sr, &hd, oh.data(), oc.data())) {
         lane.searchPhase(sr);
