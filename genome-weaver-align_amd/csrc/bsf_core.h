@@ -157,7 +157,12 @@ GWA_HD uint64_t kmerInterval(const OccBlock *occ, const uint64_t C[5], uint64_t 
 // Per-lane search state (SearchState, S/BidirectionalSuffixFilter.java:658-877)
 // ---------------------------------------------------------------------------------------------
 enum : uint8_t { SI_FWD = 0, SI_BWD = 1, SI_BID = 2, SI_EMPTY = 3 };
-enum : uint8_t { M_SIVALID = 4, M_CURVALID = 8, M_NFAVALID = 16 };
+enum : uint8_t { M_SIVALID = 4, M_CURVALID = 8, M_NFAVALID = 16, M_TEXT = 32 };
+// Text mode (M_TEXT, BsfLane::nextSi): the state's pattern P occurs exactly once in the cyclic text,
+// so every interval of its SiSet is one row or empty and is decided by one text character.  The
+// SiSet then holds lb[0] = t, the text start of P (strand 0) or of reverse(P) (strand 1; the read
+// complement is matched reversed, A/FMIndexOnGenome.java:134-146), lb[1] = |P|, lb[2] = the one
+// character c whose SiSet entry is non-empty (4 = none).
 enum : int { D_FORWARD = 0, D_BACKWARD = 1, D_BIFWD = 2 };
 
 template <int R>
@@ -548,9 +553,16 @@ struct BsfLane {
   GWA_HD static uint8_t siType(const DState<R> &s) { return s.meta & 3; }
   GWA_HD static bool siValid(const DState<R> &s) { return (s.meta & M_SIVALID) != 0; }
   // getForward(ch): returns false for null
+  GWA_HD static bool siText(const DState<R> &s) { return (s.meta & M_TEXT) != 0; }
+  // (in text mode the returned interval is the dummy one-row [0, 1): its rows are never read)
   GWA_HD static bool siGetF(const DState<R> &s, int ch, uint32_t *lb, uint32_t *ub) {
     uint8_t t = siType(s);
     if (!siValid(s) || (t != SI_FWD && t != SI_BID)) return false;
+    if (siText(s)) {
+      if ((int)s.lb[2] != ch) return false;
+      *lb = 0; *ub = 1;
+      return true;
+    }
     const uint32_t l = pick(s.lb, ch), u = pick(s.ub, ch);
     if (l >= u) return false;
     *lb = l; *ub = u;
@@ -559,6 +571,11 @@ struct BsfLane {
   GWA_HD static bool siGetB(const DState<R> &s, int ch, uint32_t *lb, uint32_t *ub) {
     uint8_t t = siType(s);
     if (!siValid(s)) return false;
+    if (siText(s)) {  // SI_BWD: c.P occurs; SI_BID: the B side of P.c, which occurs iff P.c does
+      if ((t != SI_BWD && t != SI_BID) || (int)s.lb[2] != ch) return false;
+      *lb = 0; *ub = 1;
+      return true;
+    }
     const uint32_t l = pick(s.lb, ch), u = pick(s.ub, ch);
     if (t == SI_BWD) {
       if (l >= u) return false;
@@ -577,10 +594,11 @@ struct BsfLane {
   GWA_HD static bool siIsEmpty(const DState<R> &s, int ch) {
     if (!siValid(s)) return true;  // NullPointerException in the reference; never reached (clipped tails)
     if (siType(s) == SI_EMPTY) return true;
+    if (siText(s)) return (int)s.lb[2] != ch;
     return pick(s.lb, ch) >= pick(s.ub, ch);
   }
   GWA_HD void siInit(DState<R> &d, int dir) {  // FMIndexOnGenome.initSet (:117-128)
-    d.meta = (uint8_t)((d.meta & ~3) | M_SIVALID | (dir == D_FORWARD ? SI_FWD : dir == D_BACKWARD ? SI_BWD : SI_BID));
+    d.meta = (uint8_t)((d.meta & ~(3 | M_TEXT)) | M_SIVALID | (dir == D_FORWARD ? SI_FWD : dir == D_BACKWARD ? SI_BWD : SI_BID));
     for (int c = 0; c < 4; ++c) {
       d.lb[c] = (uint32_t)ix.C[c];
       d.ub[c] = (uint32_t)ix.C[c + 1];
@@ -1195,10 +1213,22 @@ struct BsfLane {
       int h = newHit(CHR_EMPTY, 0, 0, 0, 0, 0, strand, nCigar, 0, 0);  // ReadHit.noHit
       return h < 0 ? -2 : h;
     }
-    // FMIndexOnGenome.toCoordinate (A/FMIndexOnGenome.java:227-238) via the full SA
+    // FMIndexOnGenome.toCoordinate (A/FMIndexOnGenome.java:227-238) via the full SA; in text mode
+    // the SA value of the one row on side fm follows from the occurrence (t, |P|) directly
     const int fm = ~(strand ^ (cFwd(d) ? 0 : 1)) & 1;
-    int64_t seqIndex = fm == 0 ? (int64_t)ix.sa[0][d.curLb] : (int64_t)ix.N - (int64_t)ix.sa[1][d.curLb];
-    ++saReads;
+    int64_t seqIndex;
+    if (siText(d)) {
+      const int64_t N = (int64_t)ix.N;
+      int64_t v = (int64_t)d.lb[0];
+      if (fm == 1) {
+        v = N - v - (int64_t)d.lb[1];
+        v = v < 0 ? v + N : v;
+      }
+      seqIndex = fm == 0 ? v : N - v;
+    } else {
+      seqIndex = fm == 0 ? (int64_t)ix.sa[0][d.curLb] : (int64_t)ix.N - (int64_t)ix.sa[1][d.curLb];
+      ++saReads;
+    }
     int64_t x = seqIndex - cOffsetOfSearchHead(d);
     const int frag = cFrag(d);
     int64_t refStart = x - k > 0 ? x - k : 0;
@@ -1328,7 +1358,43 @@ struct BsfLane {
     if (cDir(c) == D_BIFWD && (int)c.cursor >= (int)c.end - 1) hasF = false;
     const int strand = cStrand(c);
     uint64_t lo[5], hi[5];
-    d.meta = (uint8_t)((d.meta & ~3) | M_SIVALID);
+    d.meta = (uint8_t)((d.meta & ~(3 | M_TEXT)) | M_SIVALID);
+    // Text mode: the child's pattern P' (P.ch when c's cursor moves forward, ch.P backward; |P'| =
+    // processed bases of c + 1) occurs once, either because P does (c in text mode) or because the
+    // interval just reached is one row (its SA value gives the occurrence).  The SiSet of P' is then
+    // the one text character next to the occurrence in the SiSet's direction.
+    if ((hasF || hasB) && (siText(c) || (cfg.textSearch && (hasF ? fu - fl : bu - bl) == 1))) {
+      const int64_t N = (int64_t)ix.N;
+      int64_t t;
+      int len;
+      if (siText(c)) {
+        len = (int)c.lb[1] + 1;
+        t = (int64_t)c.lb[0];
+        // strand 0 prepends (backward) and strand 1 appends (forward) at the text start
+        if ((strand == 0) != cFwd(c)) t = t == 0 ? N - 1 : t - 1;
+      } else {
+        len = cProcessed(c) + 1;
+        const int fm = hasF ? (strand == 0 ? 1 : 0) : (strand == 0 ? 0 : 1);
+        const int64_t v = (int64_t)ix.sa[fm][hasF ? fl : bl];
+        ++saReads;
+        // fm 0 (T) rows start at t; fm 1 (reverse(T)) rows start at N - t - |P'|
+        t = fm == 0 ? v : N - v - len;
+        t = t < 0 ? t + N : t;
+      }
+      // the next character: after the occurrence for a forward SiSet on strand 0 / a backward one
+      // on strand 1, before it otherwise
+      const bool after = (strand == 0) == hasF;
+      int64_t p = after ? t + len : t - 1;
+      p = p >= N ? p - N : p < 0 ? p + N : p;
+      d.meta |= M_TEXT | (hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD);
+      d.lb[0] = (uint32_t)t;
+      d.lb[1] = (uint32_t)len;
+      d.lb[2] = (uint32_t)refCode(p);
+      d.lb[3] = 0;
+      for (int i = 0; i < 4; ++i) d.ub[i] = 0;
+      d.bBase = 0;
+      return;
+    }
     if (hasF) {
       const int fm = strand == 0 ? 1 : 0;
       rank2(fm, fl, fu, lo, hi);
@@ -1355,50 +1421,6 @@ struct BsfLane {
     d.meta |= SI_EMPTY;
     for (int i = 0; i < 4; ++i) d.lb[i] = d.ub[i] = 0;
     d.bBase = 0;
-  }
-
-  // SearchState.nextState (:840-852); returns new state index, -1 = null, -2 = overflow
-  GWA_HD int nextState(int c, int ch) {
-    const DState<R> cs = S(c);
-    const int strand = cStrand(cs);
-    uint64_t rows[R];
-    int nh = 0, nko = 0;
-    bool hm = false;
-    // the FM step (next(c, ch)) happens first in the reference (:422-424)
-    DState<R> d;
-    d.meta = 0;
-    nextSi(cs, ch, d);
-    ++numFMIndexSearches;
-    tr(2, (uint32_t)ch, d.lb[0] ^ (d.ub[1] * 3u) ^ (d.lb[2] * 7u) ^ (d.ub[3] * 11u) ^ d.bBase, (uint32_t)(d.meta & 3));
-    GWA_PT(tq);
-    const bool nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm);
-    GWA_PA(PR_NFA, tq);
-    if (!nfaOk) { tr(3, 0, 0, 0); return -1; }
-    tr(4, (uint32_t)nh | ((uint32_t)nko << 8) | ((uint32_t)hm << 16), (uint32_t)rows[0], (uint32_t)(nh > 1 ? rows[1] : 0));
-    int id = allocState();
-    if (id < 0) return -2;
-    // Cursor.next (S/Cursor.java:158-180)
-    int nc = cs.cursor, dir = cDir(cs);
-    if (dir == D_FORWARD) ++nc;
-    else if (dir == D_BACKWARD) --nc;
-    else {
-      if (nc + 1 < cs.end) ++nc;
-      else { dir = D_BACKWARD; nc = cs.pivot; }
-    }
-    setCursor(d, strand, dir, cs.start, cs.end, nc, cs.pivot);
-    uint32_t sl = 0, su = 0;
-    bool sv = dir != D_BACKWARD ? siGetF(cs, ch, &sl, &su) : siGetB(cs, ch, &sl, &su);
-    d.curLb = sv ? sl : 0;
-    d.curUb = sv ? su : 0;
-    if (sv) d.meta |= M_CURVALID;
-    d.meta |= M_NFAVALID;
-    d.state = packState(ch, nko, prio(c), hm);
-    d.nextSplit = cs.nextSplit;
-    d.nrows = (uint8_t)nh;
-    d.kOffset = (uint8_t)nko;
-    for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
-    S(id) = d;
-    return id;
   }
 
   // nextStateAfterSplit / nextStateAfterClipping (:803-838); -1 null, -2 overflow

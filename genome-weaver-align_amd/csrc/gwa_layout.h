@@ -73,6 +73,9 @@ struct SearchConfig {
   // scheduler (not a reference option): a wavefront runs its parked reports once they are at least
   // waitQ16/16 of its live lanes
   int32_t waitQ16;
+  // 1: search states whose pattern occurs once step by text compares (M_TEXT).  Exact for
+  // numSplit <= 1, where no split changes a state's search direction (BsfLane::nextSi)
+  int32_t textSearch;
 };
 
 // Read batch as resident in HBM: one byte code (0..4) per base; every read starts at a 16-B

@@ -137,6 +137,8 @@ int hc_align(void *p, float k, int reportType, int numSplit, uint32_t n, const c
   SearchConfig cfg{};
   cfg.k = k; cfg.reportType = reportType; cfg.topL = 5; cfg.numSplit = numSplit;
   cfg.matchScore = 1; cfg.mismatchPenalty = 3; cfg.splitOpenPenalty = 11; cfg.indelEndSkip = 5; cfg.bandWidth = 31;
+  cfg.waitQ16 = 16;
+  cfg.textSearch = (numSplit <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;  // as gwa_batch_create
   std::vector<int> lens;
   int kmax = 0;
   for (uint32_t i = 0; i < n; ++i) {
