@@ -186,6 +186,7 @@ struct DHit {
 // per-lane scratch capacities (entries)
 struct Caps {
   int32_t arena, heap, hits, list, cigar, dpWords, path, wr;
+  int32_t cand;  // SuffixFilter candidate set (sf_core.h); 0 on the BSF path
 };
 
 // Per-lane scratch.  The search structures (arena/heap/hits/list/cigar) sit in a per-lane slice;
@@ -197,7 +198,7 @@ struct LaneMem {
   // two base pointers + uniform offsets (kept in SGPRs), not eight per-lane pointers
   uint8_t *slice;          // this lane's slice: arena | heap | hits | list | cigar
   uint8_t *chunk;          // interleaved block (the wavefront's on the GPU, the lane's on the host)
-  uint32_t oHeap, oHits, oList, oCigar;  // byte offsets in the slice
+  uint32_t oHeap, oCand, oHits, oList, oCigar;  // byte offsets in the slice
   uint32_t oWr, oPath;     // byte offsets of the wr / path planes in the chunk
   int lane, is;            // lane in the interleaved block, interleave stride (elements)
   // PriorityQueue array of (key << 16 | state index): entry i at heapP[i * hs].  In the slice
@@ -206,6 +207,7 @@ struct LaneMem {
   int hs;
   GWA_HD DState<R> *arena() const { return (DState<R> *)slice; }
   GWA_HD uint64_t *heap() const { return heapP; }
+  GWA_HD int64_t *cand() const { return (int64_t *)(slice + oCand); }
   GWA_HD DHit *hits() const { return (DHit *)(slice + oHits); }
   GWA_HD int32_t *list() const { return (int32_t *)(slice + oList); }
   GWA_HD uint16_t *cigar() const { return (uint16_t *)(slice + oCigar); }
@@ -219,6 +221,7 @@ GWA_HD size_t laneBytes(const Caps &c) {  // per-lane slice
   size_t b = 0;
   b += sizeof(DState<R>) * (size_t)c.arena;
   b += 8 * (size_t)c.heap;
+  b += 8 * (size_t)c.cand;
   b += sizeof(DHit) * (size_t)c.hits;
   b += 4 * (size_t)c.list;
   b += 2 * (size_t)c.cigar;
@@ -236,6 +239,7 @@ GWA_HD LaneMem<R> laneMem(uint8_t *slice, uint8_t *chunk, int laneInWave, int is
   size_t b = sizeof(DState<R>) * (size_t)c.arena;
   L.slice = slice;
   L.oHeap = (uint32_t)b; b += 8 * (size_t)c.heap;
+  L.oCand = (uint32_t)b; b += 8 * (size_t)c.cand;
   L.oHits = (uint32_t)b; b += sizeof(DHit) * (size_t)c.hits;
   L.oList = (uint32_t)b; b += 4 * (size_t)c.list;
   L.oCigar = (uint32_t)b;
@@ -308,7 +312,7 @@ struct BsfLane {
   int nStates, heapSize, nHits, listSize, nCigar;
   int status;  // ST_*
   // instrumentation
-  int quickSteps, blocks, saReads, maxHeap, kmerLookups, shortSteps;
+  int quickSteps, blocks, saReads, maxHeap, kmerLookups, shortSteps, textSteps;
   // debug trace (nullptr in production launches): 4 words per event
   uint32_t *trace = nullptr;
   int traceCap = 0, traceN = 0;
@@ -443,17 +447,25 @@ struct BsfLane {
   uint64_t qwH[2 * QW];
   GWA_HD void hostWords() { qwL = qwH; qwS = 1; }
 #endif
-  GWA_HD void buildMasks() {
+  GWA_HD int buildMasks() {  // returns the read's N count
 #if !defined(__HIP_DEVICE_COMPILE__)
     hostWords();
 #endif
     uint64_t v0[QW], v1[QW];
-    loadWords(v0, v1);
+    const int countN = loadWords(v0, v1);
 #pragma unroll
     for (int w = 0; w < QW; ++w) {
       qwL[(size_t)w * qwS] = v0[w];
       qwL[(size_t)(QW + w) * qwS] = v1[w];
     }
+    return countN;
+  }
+  // qWindow over the LDS words (search kernels)
+  GWA_HD uint32_t qWindowL(int strand, int i, int K) const {
+    const int w = i >> 5, sh = 2 * (i & 31);
+    const uint64_t a = qword(strand, w), b = qword(strand, w + 1);
+    const uint64_t x = sh ? (a >> sh) | (b << (64 - sh)) : a;
+    return (uint32_t)(x & ((1ULL << (2 * K)) - 1ULL));
   }
   GWA_HD uint64_t qword(int strand, int w) const {
     return (unsigned)w < (unsigned)QW ? (uint64_t)qwL[(size_t)(strand * QW + w) * qwS] : 0ULL;
@@ -1280,11 +1292,14 @@ struct BsfLane {
   GWA_HD bool nfaNext(const DState<R> &s, int ch, int strand, uint64_t (&outRows)[R], int *outH, int *outKOff, bool *hasMatch) {
     const int height = s.nrows;
     const int kOff = s.kOffset;
-    const int kk = kOff + height - 1;
-    const int kr = kk - kOff;
+    const int kr = height - 1;
     const int64_t qeq = patternMask64(strand, cFwd(s), cNextIdx(s), s.pivot, s.cursor, ch, kr);
-    const int progress = cProcessed(s);
-    const int frag = cFrag(s);
+    return nfaCore(s.nfa, height, kOff, qeq, cProcessed(s), cFrag(s), outRows, outH, outKOff, hasMatch);
+  }
+  // ReadAlignmentNFA.nextState(qeq, progressIndex, fragmentLength, ...) (S/ReadAlignmentNFA.java:146-203)
+  GWA_HD bool nfaCore(const uint64_t (&nfa)[R], int height, int kOff, int64_t qeq, int progress, int frag,
+                      uint64_t (&outRows)[R], int *outH, int *outKOff, bool *hasMatch) {
+    const int kk = kOff + height - 1;
     const int soff = progress - kk;
     int64_t next[R];
     int minKwithMatch = kk + 1, minKwithProgress = kk + 1;
@@ -1294,7 +1309,7 @@ struct BsfLane {
     for (int i = 0; i < R; ++i) {
       next[i] = 0;
       if (i < height) {
-        const int64_t a = (int64_t)s.nfa[i];
+        const int64_t a = (int64_t)nfa[i];
         int64_t nx = jshl(a & qeq, 1);
         if (i == 0) {
           if (nx != 0) { minKwithMatch = 0; minKwithProgress = 0; }
@@ -1327,7 +1342,7 @@ struct BsfLane {
     // removeLayersFromAutomaton (:205-215): the OLD rows when nothing is trimmed
     if (rem == 0) {
 #pragma unroll
-      for (int i = 0; i < R; ++i) outRows[i] = s.nfa[i];
+      for (int i = 0; i < R; ++i) outRows[i] = nfa[i];
       *outH = height;
     } else {
       const int nh = height - rem;
@@ -1386,6 +1401,7 @@ struct BsfLane {
       const bool after = (strand == 0) == hasF;
       int64_t p = after ? t + len : t - 1;
       p = p >= N ? p - N : p < 0 ? p + N : p;
+      ++textSteps;
       d.meta |= M_TEXT | (hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD);
       d.lb[0] = (uint32_t)t;
       d.lb[1] = (uint32_t)len;
@@ -1515,6 +1531,7 @@ struct BsfLane {
     oh->states = 0;
     oh->searchBlocks = 0;
     oh->saReads = 0;
+    oh->searchShort = 0;
     oh->nChains = oh->nHits = oh->nCigar = 0;
     oh->status = ST_UNMAPPED;
     {
@@ -1795,13 +1812,14 @@ struct BsfLane {
       stairInLds = (stairLds != nullptr && m == st.ldsM) ? 1 : 0;
       stairTab = st.tab + (stairBad ? 0 : b);
     }
-    quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = 0;
+    quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = textSteps = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains
   GWA_HD void writeSearchOutput(OutHeader *oh, OutHit *oHits, uint16_t *oCig, int outHitCap, int outCigCap) {
     oh->fmSearches = numFMIndexSearches;
     oh->searchBlocks = blocks;
     oh->saReads = saReads;
+    oh->searchShort = textSteps;
     oh->states = nStates;
     oh->maxHeap = maxHeap;
     oh->nChains = 0;

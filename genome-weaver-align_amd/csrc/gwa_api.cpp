@@ -95,6 +95,7 @@ struct gwa_batch {
   OutHit *d_hits = nullptr;
   uint16_t *d_cig = nullptr;
   uint32_t *d_list[2] = {nullptr, nullptr};
+  uint32_t *d_all = nullptr;    // -m sf: every read (0..n-1) is searched
   uint32_t *d_count = nullptr;  // [0] search list, [1..] overflow lists
   uint64_t *d_stair = nullptr;
   uint32_t *d_stairBase = nullptr;
@@ -296,7 +297,7 @@ void gwa_index_close(gwa_index_t *ix) {
 void gwa_free(void *p) { free(p); }
 
 static void freeBatchDev(gwa_batch *b) {
-  void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_count,
+  void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
                 b->d_stair, b->d_stairBase};
   for (void *p : ps)
     if (p) (void)hipFree(p);
@@ -305,7 +306,8 @@ static void freeBatchDev(gwa_batch *b) {
 int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_batch_t **out) {
   auto *b = new gwa_batch();
   try {
-    if (cfg->strategy != 0) throw std::runtime_error("only -m bsf is implemented on the device path");
+    if (cfg->strategy != 0 && cfg->strategy != 1)
+      throw std::runtime_error("only -m bsf and -m sf are implemented on the device path");
     HIPCHK(hipSetDevice(ix->device));
     b->ix = ix;
     b->cfg = *cfg;
@@ -385,6 +387,11 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     b->d_list[0] = devAlloc<uint32_t>(n);
     b->d_list[1] = devAlloc<uint32_t>(n);
     b->d_count = devAlloc<uint32_t>(8);
+    if (cfg->strategy == 1) {
+      std::vector<uint32_t> all(n);
+      for (uint32_t i = 0; i < n; ++i) all[i] = i;
+      b->d_all = devUpload(all, s, nullptr);
+    }
     HIPCHK(hipStreamSynchronize(s));
     *out = b;
     return 0;
@@ -395,15 +402,21 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
   }
 }
 
-// capacity tiers: (arena, heap, hits, list, cigar) and the lane budget of each tier
+// capacity tiers: (arena, heap, hits, list, cigar, candidates) and the lane budget of each tier
 struct Tier {
-  int arena, heap, hits, list, cigar;
+  int arena, heap, hits, list, cigar, cand;
   uint32_t maxLanes;
 };
 static const Tier kTiers[3] = {
-    {256, kLdsHeap, 32, 32, 512, 256u * 1024u},  // heap in LDS
-    {4096, 4096, 256, 256, 4096, 16384u},
-    {65536, 65536, 4096, 4096, 65536, 1024u},
+    {256, kLdsHeap, 32, 32, 512, 0, 256u * 1024u},  // heap in LDS
+    {4096, 4096, 256, 256, 4096, 0, 16384u},
+    {65536, 65536, 4096, 4096, 65536, 0, 1024u},
+};
+// -m sf: no quick-scan exit, every read starts with up to 2 (k + 2) seeds; heap in the slice
+static const Tier kSfTiers[3] = {
+    {512, 512, 32, 32, 512, 32, 128u * 1024u},
+    {8192, 8192, 256, 256, 4096, 1024, 16384u},
+    {65536, 65536, 4096, 4096, 65536, 16384, 1024u},
 };
 
 int gwa_batch_run(gwa_batch_t *b) {
@@ -419,11 +432,13 @@ int gwa_batch_run(gwa_batch_t *b) {
     HIPCHK(hipEventCreate(&e2));
     HIPCHK(hipMemsetAsync(b->d_count, 0, 8 * sizeof(uint32_t), s));
     HIPCHK(hipEventRecord(e0, s));
-    const char *qtre = getenv("GWA_QTRACE_READ");
+    const bool sf = b->cfg.strategy == 1;
+    const char *qtre = sf ? nullptr : getenv("GWA_QTRACE_READ");
     static uint32_t *d_qtrace = nullptr;
     if (qtre && !d_qtrace) { HIPCHK(hipMalloc(&d_qtrace, 4 * 65540)); HIPCHK(hipMemset(d_qtrace, 0, 4 * 65540)); }
-    launchQuickscan(b->maxM <= 128 ? 4 : 8, ix->view, b->scfg, rv, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, b->d_list[0],
-                    b->d_count, s, qtre ? d_qtrace : nullptr, qtre ? atoi(qtre) : -1);
+    if (!sf)
+      launchQuickscan(b->maxM <= 128 ? 4 : 8, ix->view, b->scfg, rv, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->hitCap,
+                      b->cigCap, b->d_list[0], b->d_count, s, qtre ? d_qtrace : nullptr, qtre ? atoi(qtre) : -1);
     if (qtre) {
       std::vector<uint32_t> tv(65537);
       HIPCHK(hipMemcpyAsync(tv.data(), d_qtrace, 4 * 65537, hipMemcpyDeviceToHost, s));
@@ -433,8 +448,8 @@ int gwa_batch_run(gwa_batch_t *b) {
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
-    uint32_t nSearch = 0;
-    HIPCHK(hipMemcpyAsync(&nSearch, b->d_count, 4, hipMemcpyDeviceToHost, s));
+    uint32_t nSearch = b->n;
+    if (!sf) HIPCHK(hipMemcpyAsync(&nSearch, b->d_count, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     float qms = 0;
     HIPCHK(hipEventElapsedTime(&qms, e0, e1));
@@ -444,9 +459,10 @@ int gwa_batch_run(gwa_batch_t *b) {
     uint32_t n = nSearch;
     const int m = std::max(b->maxM, 1);
     for (int t = 0; t < 3 && n > 0; ++t) {
-      const Tier &T = kTiers[t];
+      const Tier &T = sf ? kSfTiers[t] : kTiers[t];
       Caps caps;
       caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
+      caps.cand = T.cand;
       const int bMax = std::max(1, (m + 63) / 64);
       const int nref = m + 2 * b->kmax + 2;
       caps.dpWords = 2 * bMax * (nref + 1);
@@ -470,6 +486,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       int traceRead = tre ? atoi(tre) : -1;
       if (traceRead >= 0 && !d_trace) { HIPCHK(hipMalloc(&d_trace, 4 * 65540)); HIPCHK(hipMemset(d_trace, 0, 4 * 65540)); }
 #ifdef GWA_PROF
+      if (sf) throw std::runtime_error("the profiling build times -m bsf only");
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
@@ -492,9 +509,14 @@ int gwa_batch_run(gwa_batch_t *b) {
         fprintf(stderr, "\n");
       }
 #else
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
-                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
-                   traceRead >= 0 ? d_trace : nullptr, traceRead);
+      if (sf)
+        launchSfSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv, t == 0 ? b->d_all : b->d_list[cur], n,
+                       ix->scratch, stride, caps, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank,
+                       b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s);
+      else
+        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
+                     b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
+                     traceRead >= 0 ? d_trace : nullptr, traceRead);
 #endif
       if (traceRead >= 0) {
         std::vector<uint32_t> tv(65537);
@@ -545,7 +567,7 @@ static int fetch(gwa_batch *b) {
   HIPCHK(hipStreamSynchronize(s));
   gwa_batch_stats_t &st = b->stats;
   st.fm_searches = st.quick_steps = st.blocks = st.states = st.quick_blocks = st.sa_reads = st.kmer_lookups = 0;
-  st.quick_short_steps = st.quick_sa_reads = 0;
+  st.quick_short_steps = st.quick_sa_reads = st.search_short_steps = 0;
   st.n_mapped = st.n_unmapped = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const OutHeader &h = b->oh[i];
@@ -557,6 +579,7 @@ static int fetch(gwa_batch *b) {
     st.sa_reads += (uint64_t)h.saReads + (uint64_t)h.quickSa;
     st.quick_sa_reads += (uint64_t)h.quickSa;
     st.quick_short_steps += (uint64_t)h.quickShort;
+    st.search_short_steps += (uint64_t)h.searchShort;
     st.states += (uint64_t)h.states;
     if (h.status == ST_MAPPED) st.n_mapped++;
     else if (h.status == ST_UNMAPPED) st.n_unmapped++;

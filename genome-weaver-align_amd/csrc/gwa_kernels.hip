@@ -9,9 +9,13 @@
 //                   (S/BidirectionalSuffixFilter.java:318-477).  R = NFA row capacity >= k+1.
 //                   Reads that exceed a capacity tier are appended to an overflow list and rerun
 //                   on a larger tier (fewer lanes, bigger slices): no CPU fallback exists.
+//   sf_search<R>  : `-m sf` (S/SuffixFilter.java), one read per lane over all reads: PrefixScan
+//                   seeds, the SFState queue and whole-read DP verification (sf_core.h); same
+//                   scratch slices and capacity tiers.
 #include <hip/hip_runtime.h>
 
 #include "bsf_core.h"
+#include "sf_core.h"
 #include "kernels.h"
 
 namespace gwa {
@@ -181,6 +185,60 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 #endif
 }
 
+// sf_search<R, QW>: persistent lanes over the read list, one read per lane per iteration (lanes take
+// reads from a shared counter, one atomic per wavefront); overflowing reads go to the next tier.
+template <int R, int QW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES)))
+sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
+                 uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig,
+                 int hitCap, int cigCap, const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = gridDim.x * blockDim.x;
+  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
+  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+  __shared__ uint64_t stairLds[kStairLdsWords];
+  if (st.ldsM >= 0) {
+    for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
+    __syncthreads();
+  }
+  __shared__ uint64_t qwLds[2 * QW * 256];
+  SfLane<R, QW> lane(ix, cfg, st, L, caps);
+  lane.chrRank = chrRank;
+  if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
+  lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
+  lane.qwS = 256;
+  for (;;) {
+    const uint64_t act = __ballot(1);
+    const int lid = __lane_id();
+    const int leader = __ffsll((long long)act) - 1;
+    uint32_t base = 0;
+    if (lid == leader) base = atomicAdd(work, (uint32_t)__popcll(act));
+    base = __shfl(base, leader);
+    const uint32_t i = base + (uint32_t)__popcll(act & ((1ULL << lid) - 1ULL));
+    if (i >= n) break;
+    const uint32_t r = list[i];
+    const int m = (int)reads.len[r];
+    OutHeader *h = oh + r;
+    bool ovf = false;
+    if (m > 32 * QW || m > 255) {
+      OutHeader z{};
+      z.status = ST_TOO_LONG;
+      *h = z;
+    } else {
+      lane.initRead(reads.codes + reads.off[r], m);
+      lane.sfSearch();
+      lane.writeSearchOutput(h, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap, hitCap, cigCap);
+      h->quickSteps = lane.quickSteps;
+      h->blocks = 0;  // (all Occ blocks are in searchBlocks on this path)
+      h->kmerLookups = lane.kmerLookups;
+      h->quickShort = lane.shortSteps;
+      h->quickSa = 0;
+      ovf = h->status == ST_OVERFLOW;
+    }
+    waveAppend(ovf, r, ovfList, ovfCount);
+  }
+}
+
 // one thread per k-mer (IndexView::kmer)
 __global__ void __launch_bounds__(256) kmer_table_kernel(const OccBlock *occ, IndexView ix, int K, uint64_t *out) {
   const uint64_t key = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -232,6 +290,31 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
     GWA_CASE2(32, 8)
 #undef GWA_CASE2
 #undef GWA_CASE
+    default: break;
+  }
+}
+
+void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                    const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
+                    const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
+                    const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s) {
+  if (n == 0) return;
+  dim3 grid((lanes + 255) / 256);
+  switch (R * 16 + QW) {
+#define GWA_SF(RR, QQ)                                                                                               \
+  case RR * 16 + QQ:                                                                                                 \
+    hipLaunchKernelGGL((sf_search_kernel<RR, QQ>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,      \
+                       laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, work, ovfList, ovfCount);       \
+    break;
+    GWA_SF(4, 4)
+    GWA_SF(4, 8)
+    GWA_SF(8, 4)
+    GWA_SF(8, 8)
+    GWA_SF(16, 4)
+    GWA_SF(16, 8)
+    GWA_SF(32, 4)
+    GWA_SF(32, 8)
+#undef GWA_SF
     default: break;
   }
 }

@@ -132,7 +132,8 @@ struct OutHeader {
   int32_t fmSearches, quickSteps, blocks, states;
   int32_t searchBlocks, saReads, maxHeap, kmerLookups;  // maxHeap: heap high-water mark (instrumentation)
   // quick-scan steps answered without Occ blocks (k-mer table or single-row text compare)
-  int32_t quickShort, quickSa, pad_[2];  // quickSa: SA gathers of the quick scan
+  int32_t quickShort, quickSa, searchShort, pad_;  // quickSa: SA gathers of the quick scan; searchShort:
+  // search FM steps answered by one text character (M_TEXT)
 };
 
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at

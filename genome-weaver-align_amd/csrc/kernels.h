@@ -18,6 +18,10 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
                   uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
                   const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s,
                   uint32_t *trace = nullptr, int traceRead = -1);
+void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                    const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
+                    const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
+                    const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s);
 void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream_t s);
 size_t laneBytesFor(int R, const Caps &c);  // per-lane slice
 size_t ilvBytesFor(const Caps &c);          // per-lane share of the interleaved DP block

@@ -41,7 +41,8 @@ class BatchStats(ctypes.Structure):
                 ("fm_searches", ctypes.c_uint64), ("quick_steps", ctypes.c_uint64), ("blocks", ctypes.c_uint64),
                 ("quick_blocks", ctypes.c_uint64), ("states", ctypes.c_uint64), ("sa_reads", ctypes.c_uint64), ("tier_reads", ctypes.c_uint32 * 4),
                 ("n_mapped", ctypes.c_uint32), ("n_unmapped", ctypes.c_uint32), ("kmer_lookups", ctypes.c_uint64),
-                ("quick_short_steps", ctypes.c_uint64), ("quick_sa_reads", ctypes.c_uint64)]
+                ("quick_short_steps", ctypes.c_uint64), ("quick_sa_reads", ctypes.c_uint64),
+                ("search_short_steps", ctypes.c_uint64)]
 
 
 _lib = None
@@ -92,7 +93,7 @@ def _check(rc):
         raise GwaError(lib().gwa_last_error().decode())
 
 
-STRATEGIES = {"bsf": 0}
+STRATEGIES = {"bsf": 0, "sf": 1}
 REPORT_TYPES = {"besthit": 0, "allhits": 1, "topl": 2}
 
 
@@ -263,6 +264,24 @@ class BidirectionalSuffixFilter:
         """Aligner.align(Read, Reporter): reporter(line) once per emitted SAM line."""
         for line in self.align_batch([read]).splitlines():
             reporter(line)
+
+
+class SuffixFilter(BidirectionalSuffixFilter):
+    """The `-m sf` Aligner (S/SuffixFilter.java), batched on one GPU."""
+
+    def __init__(self, fmIndex, config=None):
+        import dataclasses
+        super().__init__(fmIndex, dataclasses.replace(config or AlignmentConfig(), strategy="sf"))
+
+
+def aligner(fmIndex, config):
+    """Align.query's strategy switch (A/Align.java:116-137): the Aligner for config.strategy."""
+    s = config.strategy.lower()
+    if s == "sf":
+        return SuffixFilter(fmIndex, config)
+    if s == "bsf":
+        return BidirectionalSuffixFilter(fmIndex, config)
+    raise GwaError("%s mode is not supported on the device path" % config.strategy)
 
 
 def reads_from_blobs(name_blob, name_off, seq_blob, seq_off, qual_blob=None, qual_off=None):

@@ -2,7 +2,7 @@
 A/AlignmentConfig.java:40-72, A/AlignmentScoreConfig.java:37-77).
 
   python genome-weaver-align_amd/gwa_cli.py align -r ref.fa [-q SEQ | reads.fq[.gz] | reads.fa[.gz]]
-         [-k 0.1] [-m bsf] [-R besthit|allhits|topL] [-L 5] [-g 1] [-e 4] [-s 1] [-M 1] [-N 3]
+         [-k 0.1] [-m bsf|sf] [-R besthit|allhits|topL] [-L 5] [-g 1] [-e 4] [-s 1] [-M 1] [-N 3]
          [-G 11] [-E 4] [-S 11] [-P 5] [-W 31] [--silent] [--device 0] [--batch 1048576]
 
 Writes SAM to stdout: the `@SQ` header (SequenceBoundary.toSAMHeader, A/SequenceBoundary.java:81-87)
@@ -116,7 +116,7 @@ def build_parser():
     a.add_argument("-q", dest="query", help="single query sequence")
     a.add_argument("readFiles", nargs="*", help="read file (single-end)")
     a.add_argument("--silent", action="store_true", help="disable output")
-    a.add_argument("-m", dest="strategy", default="bsf", help="alignment strategy (bsf)")
+    a.add_argument("-m", dest="strategy", default="bsf", help="alignment strategy: bsf (default), sf")
     a.add_argument("-R", dest="reportType", default="besthit", help="besthit (default), allhits, topL")
     a.add_argument("-L", dest="topL", type=int, default=5)
     a.add_argument("-k", dest="k", type=float, default=0.1,
@@ -154,7 +154,7 @@ def align(ns, out=sys.stdout):
         raise gwa.GwaError("# of input read files must be one (single-end)")
     cfg = config_of(ns)
     fm = gwa.FMIndexOnGenome.load(ns.refSeq, device=ns.device)
-    bsf = gwa.BidirectionalSuffixFilter(fm, cfg)
+    bsf = gwa.aligner(fm, cfg)
     w = (lambda s: None) if ns.silent else out.write
     w(fm.samHeader())
     src = iter([("read", ns.query, None)]) if ns.query is not None else reads_of(ns.readFiles[0])

@@ -2,7 +2,7 @@
  *
  * Replaces, for the single-end FM-index path, the reference's Java plugin surface:
  *   interface Aligner { void align(Read read, Reporter out) }      A/Aligner.java:30-33
- *   Align.query(...) strategy selection (-m bsf)                     A/Align.java:112-140
+ *   Align.query(...) strategy selection (-m bsf, -m sf)              A/Align.java:112-140
  *   Reporter.emit -> SAMOutput.emit -> AlignmentRecord.toSAMLine     J/parallel/Reporter.java:27-30,
  *                                                                    A/SAMOutput.java:73-82
  *   FMIndexOnGenome.load / buildFromSequence                         A/FMIndexOnGenome.java:60-115
@@ -30,7 +30,7 @@ typedef struct gwa_batch gwa_batch_t;
  * defaults from gwa_config_default: k 0.1, bsf, besthit, L 5, g 1, e 4, s 1, M 1, N 3, G 11, E 4, S 11, P 5, W 31 */
 typedef struct {
   float k;
-  int32_t strategy;    /* 0 = bsf (-m bsf); others are rejected */
+  int32_t strategy;    /* 0 = bsf (-m bsf), 1 = sf (-m sf, S/SuffixFilter.java); others are rejected */
   int32_t report_type; /* 0 besthit, 1 allhits, 2 topL (-R) */
   int32_t top_l;       /* -L */
   int32_t num_gap_open, num_gap_ext, num_split; /* -g -e -s */
@@ -71,6 +71,7 @@ typedef struct {
   uint64_t kmer_lookups;   /* 8-B k-mer interval-table reads by fm_quickscan */
   uint64_t quick_short_steps; /* FMQuickScan steps answered without Occ blocks (k-mer table, single-row text compare) */
   uint64_t quick_sa_reads; /* of sa_reads, by fm_quickscan */
+  uint64_t search_short_steps; /* search FM steps answered by one text character (single-row states) */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);

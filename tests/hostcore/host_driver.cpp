@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../genome-weaver-align_amd/csrc/bsf_core.h"
+#include "../../genome-weaver-align_amd/csrc/sf_core.h"
 #include "../../genome-weaver-align_amd/csrc/host_index.h"
 #include "../../genome-weaver-align_amd/csrc/sam.h"
 
@@ -22,14 +23,17 @@ struct HC {
 
 // the GPU's capacity tiers (gwa_api.cpp kTiers) replayed on the CPU
 template <int R, int QW>
-static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int maxM, int kmax, uint32_t n,
+static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTables &st, int maxM, int kmax, uint32_t n,
                   const char *const *names, const char *const *seqs, const char *const *quals, std::string &sam,
                   int32_t *stats) {
   const int bMax = std::max(1, (maxM + 63) / 64), nref = maxM + 2 * kmax + 2;
   const int dpw = 2 * bMax * (nref + 1), path = maxM + nref + 8, wrn = nref + 2;
-  const Caps tiers[3] = {{256, kLdsHeap, 32, 32, 512, dpw, path, wrn}, {4096, 4096, 256, 256, 4096, dpw, path, wrn},
-                         {65536, 65536, 4096, 4096, 65536, dpw, path, wrn}};
-  std::vector<uint8_t> scratch(laneBytes<R>(tiers[2]) + ilvBytes(tiers[2]) + 4096);
+  const Caps tiers[3] = {{256, kLdsHeap, 32, 32, 512, dpw, path, wrn, 0}, {4096, 4096, 256, 256, 4096, dpw, path, wrn, 0},
+                         {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 0}};
+  // -m sf tiers (gwa_api.cpp kSfTiers)
+  const Caps sfTiers[3] = {{512, 512, 32, 32, 512, dpw, path, wrn, 32}, {8192, 8192, 256, 256, 4096, dpw, path, wrn, 1024},
+                           {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 16384}};
+  std::vector<uint8_t> scratch(std::max(laneBytes<R>(tiers[2]), laneBytes<R>(sfTiers[2])) + ilvBytes(tiers[2]) + 4096);
   const int chains = cfg.reportType == 0 ? 1 : 4;
   const int hitCap = chains * (cfg.numSplit + 1), cigCap = 64 * chains;
   std::vector<OutHit> oh(hitCap);
@@ -45,6 +49,18 @@ static int runAll(HC *x, const SearchConfig &cfg, const StairTables &st, int max
     std::vector<uint32_t> tv(65537, 0);
     bool traced = false;
     for (int t = 0; t < 3; ++t) {
+      if (strategy == 1) {
+        LaneMem<R> L = laneMem<R>(scratch.data(), sfTiers[t]);
+        SfLane<R, QW> lane(x->v, cfg, st, L, sfTiers[t]);
+        lane.chrRank = rk.data();
+        lane.initRead(codes.data(), (int)mlen);
+        hd = OutHeader{};
+        lane.sfSearch();
+        lane.writeSearchOutput(&hd, oh.data(), oc.data(), hitCap, cigCap);
+        hd.quickSteps = lane.quickSteps;
+        if (hd.status != ST_OVERFLOW) break;
+        continue;
+      }
       LaneMem<R> L = laneMem<R>(scratch.data(), tiers[t]);
       BsfLane<R, QW> lane(x->v, cfg, st, L, tiers[t]);
       lane.chrRank = rk.data();
@@ -131,7 +147,7 @@ int hc_sa(void *p, int strand, uint32_t *out) {
 }
 
 // Align with the kernel logic on the CPU; output SAM text (malloc'd).  stats[i*4..] = fm, quick, max heap, states
-int hc_align(void *p, float k, int reportType, int numSplit, uint32_t n, const char *const *names, const char *const *seqs,
+int hc_align(void *p, float k, int reportType, int numSplit, int strategy, uint32_t n, const char *const *names, const char *const *seqs,
              const char *const *quals, char **out, uint64_t *outLen, int32_t *stats) {
   auto *x = (HC *)p;
   SearchConfig cfg{};
@@ -158,10 +174,10 @@ int hc_align(void *p, float k, int reportType, int numSplit, uint32_t n, const c
   int R = kmax + 1 <= 4 ? 4 : kmax + 1 <= 8 ? 8 : kmax + 1 <= 16 ? 16 : 32;
   int rc = 0;
   switch (R) {
-    case 4: rc = (maxM <= 128 ? runAll<4, 4> : runAll<4, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    case 8: rc = (maxM <= 128 ? runAll<8, 4> : runAll<8, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    case 16: rc = (maxM <= 128 ? runAll<16, 4> : runAll<16, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    default: rc = (maxM <= 128 ? runAll<32, 4> : runAll<32, 8>)(x, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 4: rc = (maxM <= 128 ? runAll<4, 4> : runAll<4, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 8: rc = (maxM <= 128 ? runAll<8, 4> : runAll<8, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 16: rc = (maxM <= 128 ? runAll<16, 4> : runAll<16, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    default: rc = (maxM <= 128 ? runAll<32, 4> : runAll<32, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
   }
   if (rc != 0) return rc;
   *out = (char *)malloc(sam.size() + 1);

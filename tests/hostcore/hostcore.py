@@ -20,7 +20,8 @@ def lib():
         L.hc_index_fasta.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
         L.hc_index_free.argtypes = [ctypes.c_void_p]
         L.hc_sa.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
-        L.hc_align.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p,
+        L.hc_align.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                               ctypes.c_void_p,
                                ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
         _lib = L
@@ -49,7 +50,7 @@ class HostCore:
         lib().hc_sa(self.h, strand, out.ctypes.data)
         return out
 
-    def align(self, reads, k=0.1, report_type=0, num_split=1, stats=False):
+    def align(self, reads, k=0.1, report_type=0, num_split=1, stats=False, strategy=0):
         n = len(reads)
         names = (ctypes.c_char_p * n)(*[r[0].encode() for r in reads])
         seqs = (ctypes.c_char_p * n)(*[r[1].encode() for r in reads])
@@ -57,7 +58,7 @@ class HostCore:
         out = ctypes.c_void_p()
         ln = ctypes.c_uint64()
         st = np.zeros(4 * n, dtype=np.int32)
-        rc = lib().hc_align(self.h, k, report_type, num_split, n, ctypes.cast(names, ctypes.c_void_p),
+        rc = lib().hc_align(self.h, k, report_type, num_split, strategy, n, ctypes.cast(names, ctypes.c_void_p),
                             ctypes.cast(seqs, ctypes.c_void_p), ctypes.cast(quals, ctypes.c_void_p), ctypes.byref(out),
                             ctypes.byref(ln), st.ctypes.data)
         if rc != 0:

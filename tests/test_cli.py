@@ -46,6 +46,8 @@ def test_options_and_errors():
     ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "-k", "2", "-R", "topL", "-L", "3", "r.fq"])
     cfg = gwa_cli.config_of(ns)
     assert cfg.k == 2.0 and cfg.reportType == "topL" and cfg.topL == 3 and cfg.bandWidth == 31
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "-m", "sf", "r.fq"])
+    assert gwa_cli.config_of(ns).strategy == "sf"
     ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "-m", "bwa", "r.fq"])
     with pytest.raises(gwa.GwaError):
         gwa_cli.config_of(ns)

@@ -30,9 +30,10 @@ def _both(codes, names, lengths):
 def _check(gi, oi, reads, **cfg):
     import gwa
     c = gwa.AlignmentConfig(**cfg)
-    got = gwa.BidirectionalSuffixFilter(gi, c).align_batch(reads)
+    got = gwa.aligner(gi, c).align_batch(reads)
     rt = {"besthit": 0, "allhits": 1, "topl": 2}[c.reportType.lower()]
-    exp = oi.align(reads, O.OrcConfig.default(k=float(c.k), report_type=rt))
+    exp = oi.align(reads, O.OrcConfig.default(k=float(c.k), report_type=rt, strategy=gwa.STRATEGIES[c.strategy],
+                                              num_split=c.numSplitAlowed))
     if got != exp:
         g, e = got.splitlines(), exp.splitlines()
         bad = [(a, b) for a, b in zip(g, e) if a != b][:3]
@@ -148,3 +149,68 @@ def test_ecoli_c1_exact(gwa):
     reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
     sam = _check(gi, oi, reads, k=0.0)
     assert all(l.split("\t")[1] in ("66", "82") for l in sam.splitlines())
+
+
+@pytest.mark.parametrize("ns", [0, 2])
+def test_num_split_other_than_one(repetitive_pair, ns):
+    # single-row text mode is off at -s 2 (exact for -s <= 1 only)
+    from test_hostcore import _mk
+    codes, gi, oi = repetitive_pair
+    _check(gi, oi, _mk(codes, 300, 100, 3, True, seed=50 + ns), k=0.1, numSplitAlowed=ns)
+
+
+# ---- -m sf (S/SuffixFilter.java) ----
+
+@pytest.mark.parametrize("k", [2.0, 0.1, 0.0])
+def test_sf_random_substitutions(random_pair, k):
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 3000, 100, 2, config_id=21)
+    strs = synth.to_strings(seqs)
+    _check(gi, oi, [(rn[i], strs[i], "I" * 100) for i in range(len(strs))], k=k, strategy="sf")
+
+
+def test_sf_indels_150_k5(random_pair):
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 500, 150, config_id=24, indels=True, max_edits=5)
+    strs = synth.to_strings(seqs)
+    _check(gi, oi, [(rn[i], strs[i], "I" * 150) for i in range(len(strs))], k=5.0, strategy="sf")
+
+
+@pytest.mark.parametrize("m,k,sub", [(100, 2.0, 2), (50, 0.1, 3)])
+@pytest.mark.parametrize("chim", [False, True])
+def test_sf_repetitive(repetitive_pair, m, k, sub, chim):
+    from test_hostcore import _mk
+    codes, gi, oi = repetitive_pair
+    _check(gi, oi, _mk(codes, 300, m, sub, chim, seed=m * 11 + int(chim)), k=k, strategy="sf")
+
+
+@pytest.mark.parametrize("rt", ["allhits", "topl"])
+def test_sf_report_modes(repetitive_pair, rt):
+    from test_hostcore import _mk
+    codes, gi, oi = repetitive_pair
+    _check(gi, oi, _mk(codes, 300, 100, 2, False, seed=77), k=2.0, reportType=rt, strategy="sf")
+
+
+def test_sf_edge_reads(random_pair):
+    codes, names, lengths, gi, oi = random_pair
+    rng = np.random.default_rng(15)
+    seqs, rn = synth.reads(codes, lengths, 300, 100, 2, config_id=25)
+    strs = synth.to_strings(seqs)
+    reads = []
+    for i in range(300):
+        s = list(strs[i])
+        for j in rng.integers(0, 100, rng.integers(0, 4)):
+            s[j] = "N"
+        reads.append(("n%d" % i, "".join(s), "I" * 100))
+    reads += [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), "I" * 100) for i in range(100)]
+    reads += [("short", "ACG", "III"), ("lower", strs[0].lower(), "I" * 100)]
+    _check(gi, oi, reads, k=2.0, strategy="sf")
+
+
+def test_sf_known_answer_queries_on_gpu(gwa):
+    # the two SuffixFilterTest queries (T/strategy/SuffixFilterTest.java:67-76) on sample3.fa
+    fa = open(os.path.join(HERE, "golden", "fixtures", "sample3.fa")).read()
+    gi, oi = gwa.FMIndexOnGenome.buildFromFasta(fa), O.Index.from_fasta(fa)
+    reads = [("exact", "CACTTTAGTATAATTGTTTTTAGTTTTTGGCAAAACTATTGTCTAAACAG", None),
+             ("insertion", "CACTTTAGTATAATTGTTTTTAGCCTTTTTGGCAAAACTATTGTCTAAACAG", None)]
+    _check(gi, oi, reads, strategy="sf")

@@ -16,11 +16,11 @@ import synth  # noqa: E402
 import hostcore  # noqa: E402
 
 
-def _cmp(codes, names, lengths, reads, k, rt=0):
+def _cmp(codes, names, lengths, reads, k, rt=0, strategy=0, num_split=1):
     oi = O.Index.from_arrays(codes, names, lengths)
     hc = hostcore.HostCore(codes, names, lengths)
-    b = oi.align(reads, O.OrcConfig.default(k=k, report_type=rt))
-    a = hc.align(reads, k=k, report_type=rt)
+    b = oi.align(reads, O.OrcConfig.default(k=k, report_type=rt, strategy=strategy, num_split=num_split))
+    a = hc.align(reads, k=k, report_type=rt, strategy=strategy, num_split=num_split)
     assert a == b
 
 
@@ -111,3 +111,62 @@ def test_reads_with_n_and_unmappable(random_genome):
     reads += [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), None) for i in range(100)]
     reads += [("e0", "", None), ("short", "ACG", None), ("lower", strs[0].lower(), None)]
     _cmp(codes, names, lengths, reads, 2.0)
+
+
+@pytest.mark.parametrize("ns", [0, 2])
+def test_num_split_other_than_one(repetitive_genome, ns):
+    # -s 0 / -s 2: single-row text mode is exact for -s <= 1 only and is off at -s 2 (bsf_core.h nextSi)
+    codes, names, lengths = repetitive_genome
+    _cmp(codes, names, lengths, _mk(codes, 150, 100, 3, True, seed=40 + ns), 0.1, num_split=ns)
+
+
+# ---- -m sf (S/SuffixFilter.java): sf_core.h on the CPU against the oracle's SuffixFilter ----
+
+@pytest.mark.parametrize("k", [2.0, 0.1, 0.0])
+def test_sf_random_genome(random_genome, k):
+    codes, names, lengths = random_genome
+    seqs, rn = synth.reads(codes, lengths, 400, 100, 2, config_id=21)
+    strs = synth.to_strings(seqs)
+    _cmp(codes, names, lengths, [(rn[i], strs[i], "I" * 100) for i in range(len(strs))], k, strategy=1)
+
+
+def test_sf_indels_150(random_genome):
+    codes, names, lengths = random_genome
+    seqs, rn = synth.reads(codes, lengths, 150, 150, config_id=24, indels=True, max_edits=5)
+    strs = synth.to_strings(seqs)
+    _cmp(codes, names, lengths, [(rn[i], strs[i], None) for i in range(len(strs))], 5.0, strategy=1)
+
+
+@pytest.mark.parametrize("m,k,sub", [(100, 2.0, 2), (50, 0.1, 3), (36, 2.0, 2)])
+@pytest.mark.parametrize("chim", [False, True])
+def test_sf_repetitive_genome(repetitive_genome, m, k, sub, chim):
+    codes, names, lengths = repetitive_genome
+    _cmp(codes, names, lengths, _mk(codes, 120, m, sub, chim, seed=m * 11 + int(chim)), k, strategy=1)
+
+
+@pytest.mark.parametrize("rt", [1, 2])
+def test_sf_report_modes(repetitive_genome, rt):
+    codes, names, lengths = repetitive_genome
+    _cmp(codes, names, lengths, _mk(codes, 120, 100, 2, False, seed=77), 2.0, rt=rt, strategy=1)
+
+
+def test_sf_reads_with_n_and_unmappable(random_genome):
+    codes, names, lengths = random_genome
+    rng = np.random.default_rng(15)
+    seqs, rn = synth.reads(codes, lengths, 120, 100, 2, config_id=25)
+    strs = synth.to_strings(seqs)
+    reads = []
+    for i in range(120):
+        s = list(strs[i])
+        for j in rng.integers(0, 100, rng.integers(0, 4)):
+            s[j] = "N"
+        reads.append(("n%d" % i, "".join(s), "I" * 100))
+    reads += [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), None) for i in range(40)]
+    reads += [("short", "ACG", None), ("lower", strs[0].lower(), None)]
+    _cmp(codes, names, lengths, reads, 2.0, strategy=1)
+    # an empty read: StaircaseFilter(0, k + 1) throws in the reference (BitVector._not), both abort
+    oi = O.Index.from_arrays(codes, names, lengths)
+    with pytest.raises(RuntimeError):
+        oi.align([("e0", "", None)], O.OrcConfig.default(k=2.0, strategy=1))
+    with pytest.raises(RuntimeError):
+        hostcore.HostCore(codes, names, lengths).align([("e0", "", None)], k=2.0, strategy=1)
