@@ -50,7 +50,13 @@ def main():
     ap.add_argument("--genome", default=os.environ.get("GWA_BENCH_GENOME", "hg19"))
     ap.add_argument("--reads", type=int, default=int(os.environ.get("GWA_BENCH_READS", "0")))
     ap.add_argument("--k", type=float, default=2.0)
-    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "20000")))
+    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "20000")),
+                    help="reads of the single-thread CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+                                                           or (os.cpu_count() or 1)),
+                    help="host threads of the multi-core CPU baseline (SURVEY.md 8(d)(ii))")
+    ap.add_argument("--cpu-sample-mt", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE_MT", "160000")),
+                    help="reads of the multi-core CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=2000, help="reads of step 0 checked against the oracle")
     args = ap.parse_args()
@@ -101,7 +107,7 @@ def main():
     t0 = time.time()
     batch = gwa.Batch(gi, cfg, blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
     log("batch resident in HBM: %.1fs" % (time.time() - t0))
-    nchk = min(max(args.check, args.cpu_sample if not args.no_cpu else 0), reads_per_step)
+    nchk = min(max(args.check, max(args.cpu_sample, args.cpu_sample_mt) if not args.no_cpu else 0), reads_per_step)
     reads = [(name_blob[10 * i:10 * i + 10].decode(), seq_blob[m * i:m * i + m].decode(), "I" * m) for i in range(nchk)]
 
     for _ in range(args.warmup):
@@ -145,7 +151,10 @@ def main():
         parity = {"reads": nchk, "identical": got == exp}
         log("parity on %d reads: %s (oracle index %.1fs)" % (nchk, got == exp, t_oidx))
 
-    cpu = None
+    # CPU baseline: the oracle (single-thread C++ restatement of the reference path) on this host.
+    # (i) 1 thread, as the reference runs (A/Align.java:174-196); (ii) T threads over contiguous read
+    # ranges.  cpu_baseline reports (ii); (i) is kept in detail.
+    cpu = cpu1 = None
     if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
@@ -155,23 +164,39 @@ def main():
         t0 = time.perf_counter()
         oi.align(reads[:ns], O.OrcConfig.default(k=args.k))
         ct = time.perf_counter() - t0
-        cpu = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port",
-               "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the reference "
-                         "BSF path (oracle/), same index" % ns}
-        log("cpu baseline: %.0f reads/s (%d reads in %.1fs)" % (ns / ct, ns, ct))
+        cpu1 = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port",
+                "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the reference "
+                          "BSF path (oracle/), same index" % ns}
+        log("cpu baseline (1 thread): %.0f reads/s (%d reads in %.1fs)" % (ns / ct, ns, ct))
+        cpu = cpu1
+        T = max(1, args.cpu_threads)
+        nt = min(args.cpu_sample_mt, len(reads))
+        if T > 1 and nt > 0:
+            t0 = time.perf_counter()
+            oi.align(reads[:nt], O.OrcConfig.default(k=args.k), threads=T)
+            ct = time.perf_counter() - t0
+            cpu = {"value": nt / ct, "unit": "reads/s", "cores": T, "kind": "port",
+                   "sample": "first %d reads of rank 0's batch on %d host threads (contiguous ranges, one "
+                             "Aligner each), C++ restatement of the reference BSF path (oracle/), same index"
+                             % (nt, T)}
+            log("cpu baseline (%d threads): %.0f reads/s (%d reads in %.1fs)" % (T, nt / ct, nt, ct))
 
-    # roofline of the dominant kernel.  Algorithmic bytes: 64 B per distinct
-    # Occ block of every reference FM step (+4 B per SA gather).  Quick-scan steps that this kernel answers
-    # without Occ blocks (k-mer table, single-row text compare) are counted at the §8d lower bound of one
-    # block per step.
+    # roofline of the dominant kernel.  Algorithmic bytes = the bytes this path's algorithm must read
+    # (DESIGN.md §5): 64 B per Occ block of every FM step that reads one, 8 B per k-mer interval-table
+    # lookup, 3/8 B (2-bit base + N bit) per FM step answered from the text (single-row interval),
+    # 4 B per suffix-array gather.  `ref_equiv_bytes` prices every reference FM step at the SURVEY.md
+    # §8d lower bound of one 64-B block instead (what the reference's algorithm would read).
     steps = args.steps
     q_ms, s_ms = qms / steps, sms / steps
-    q_bytes = 64.0 * (st.quick_blocks + st.quick_short_steps) + 4.0 * st.quick_sa_reads
-    s_bytes = 64.0 * (st.blocks - st.quick_blocks) + 4.0 * (st.sa_reads - st.quick_sa_reads)
+    q_bytes = 64.0 * st.quick_blocks + 8.0 * st.kmer_lookups + 0.375 * st.quick_short_steps + 4.0 * st.quick_sa_reads
+    q_ref = 64.0 * (st.quick_blocks + st.quick_short_steps) + 4.0 * st.quick_sa_reads
+    s_bytes = (64.0 * (st.blocks - st.quick_blocks) + 0.375 * st.search_short_steps
+               + 4.0 * (st.sa_reads - st.quick_sa_reads))
+    s_ref = 64.0 * (st.blocks - st.quick_blocks + st.search_short_steps) + 4.0 * (st.sa_reads - st.quick_sa_reads)
     if q_ms >= s_ms:
-        dom, ach_bytes, dom_ms = "fm_quickscan", q_bytes, q_ms
+        dom, ach_bytes, dom_ms, dom_ref = "fm_quickscan", q_bytes, q_ms, q_ref
     else:
-        dom, ach_bytes, dom_ms = "bsf_search", s_bytes, s_ms
+        dom, ach_bytes, dom_ms, dom_ref = "bsf_search", s_bytes, s_ms, s_ref
     achieved = ach_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     workload = ("%s; %d x 100 bp reads per GPU per step, 0-2 substitutions, -k %g, -m bsf, besthit"
                 % (gname, reads_per_step, args.k))
@@ -185,15 +210,18 @@ def main():
                    "parallelism": "reads sharded, index replicated (%d GPU)" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": ach_bytes, "avg_launch_ms": dom_ms},
+                     "algorithmic_bytes_per_launch": ach_bytes, "avg_launch_ms": dom_ms,
+                     "ref_equiv_bytes_per_launch": dom_ref},
         "cpu_baseline": cpu,
         "detail": {"quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
                    "fm_searches_per_read": st.fm_searches / reads_per_step,
                    "quick_steps_per_read": st.quick_steps / reads_per_step,
                    "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
                    "quick_short_steps_per_read": st.quick_short_steps / reads_per_step,
+                   "cpu_baseline_1thread": cpu1,
+                   "search_short_steps_per_read": st.search_short_steps / reads_per_step,
                    "rank_kernel": {"kernel": "fm_quickscan", "algorithmic_bytes_per_launch": q_bytes,
-                                   "avg_launch_ms": q_ms,
+                                   "ref_equiv_bytes_per_launch": q_ref, "avg_launch_ms": q_ms,
                                    "achieved_GBs": q_bytes / (q_ms * 1e-3) / 1e9 if q_ms > 0 else 0.0,
                                    "frac": (q_bytes / (q_ms * 1e-3) / 1e9 if q_ms > 0 else 0.0) / HBM_PEAK_GBS,
                                    "traffic": _pmc_traffic("fm_quickscan", workload)[0]},

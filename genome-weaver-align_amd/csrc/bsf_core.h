@@ -1029,9 +1029,25 @@ struct BsfLane {
   }
 
   // BitParallelSmithWaterman.alignBlockDetailed (A/BitParallelSmithWaterman.java:141-147,394-644).
-  // The live column (<=4 blocks of 64 rows) stays in VGPRs; the vp/vn history the traceback needs
-  // is written to HBM scratch, with one byte per column recording which cells were written
-  // (cells never written read as 0, as the reference's zero-initialised long[][] do).
+  // The live column (<=4 blocks of 64 rows) stays in VGPRs.  The vp/vn history the traceback needs
+  // goes to HBM scratch as one 16-B {vp, vn} pair per (column, block) -- one dwordx4 store per block
+  // per column, 64 lanes of a wavefront adjacent -- and the per-column write record (bits 0-3
+  // computed, 4-7 activated-as-input; cells never written read as 0, as the reference's
+  // zero-initialised long[][] do) is packed 4 columns to a u32 and stored once per 4 columns.
+  struct alignas(16) VpVn { uint64_t vp, vn; };
+  // Peq of the DP query (the fragment q[strand][qs, qe), reversed on strand 1, :532-534) for block r
+  // and base ch: bit j = (query[64 r + j] == ch), from the 2-bit read words (eqWindow), not per base
+  GWA_HD uint64_t dpPeq(int strand, int qs, int qe, int r, int ch) const {
+    const int mq = qe - qs, rows = mq - 64 * r;
+    uint64_t x;
+    if (strand == 0) {
+      x = eqWindow(0, ch, qs + 64 * r);
+    } else {
+      const int len = qe - 64 * r;  // positions [0, len) of strand 1 precede this block's first row
+      x = len >= 64 ? bitrev64(eqWindow(1, ch, len - 64)) : bitrev64(eqWindow(1, ch, 0) << (64 - len));
+    }
+    return rows >= 64 ? x : (x & ((1ULL << rows) - 1ULL));
+  }
   GWA_HD int alignBlockDetailed(int strand, int qs, int qe, int64_t refStart, int64_t refEnd, int *outPos, int *outDiff,
                                 int *cigOff, int *cigLen) {
     const int w = 64;
@@ -1039,26 +1055,19 @@ struct BsfLane {
     const int kb = cfg.bandWidth;
     const int bMax = mq + w - 1 >= w ? (mq + w - 1) / w : 1;
     const int N = (int)(refEnd - refStart);
-    if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || mq + N + 2 > caps.path || N + 1 > caps.wr) { status = ST_OVERFLOW; return -1; }
-    uint64_t pA[DB] = {}, pC[DB] = {}, pG[DB] = {}, pT[DB] = {};
-    for (int p = 0; p < mq; ++p) {
-      const int c = dpQ(strand, qs, qe, p);
-      const uint64_t bit = 1ULL << (p & 63);
-      const int b = p >> 6;
+    if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || 4 * ((N >> 2) + 1) > caps.wr) { status = ST_OVERFLOW; return -1; }
+    uint64_t pA[DB], pC[DB], pG[DB], pT[DB];
 #pragma unroll
-      for (int r = 0; r < DB; ++r) {
-        if (r == b) {
-          if (c == 0) pA[r] |= bit;
-          else if (c == 1) pC[r] |= bit;
-          else if (c == 2) pG[r] |= bit;
-          else pT[r] |= bit;
-        }
-      }
+    for (int r = 0; r < DB; ++r) {
+      const bool on = r < bMax;
+      pA[r] = on ? dpPeq(strand, qs, qe, r, 0) : 0ULL;
+      pC[r] = on ? dpPeq(strand, qs, qe, r, 1) : 0ULL;
+      pG[r] = on ? dpPeq(strand, qs, qe, r, 2) : 0ULL;
+      pT[r] = on ? dpPeq(strand, qs, qe, r, 3) : 0ULL;
     }
     const size_t is = (size_t)L.is;
-    uint64_t *hvp = L.dp();                          // [col 1..N][block] history
-    uint64_t *hvn = L.dp() + is * bMax * (N + 1);
-    uint8_t *wr = L.wr();                            // per column: bits 0-3 computed, bits 4-7 activated-as-input
+    VpVn *hist = (VpVn *)L.chunk + L.lane;                      // [col 0..N][block] history
+    uint32_t *wr = (uint32_t *)(L.chunk + L.oWr) + L.lane;      // [col / 4] write records, byte col % 4
     uint64_t vp[DB], vn[DB];
     int D[DB] = {}, sb[DB];
 #pragma unroll
@@ -1069,6 +1078,7 @@ struct BsfLane {
       sb[r] = v > 0 ? v : 0;
     }
     uint32_t pend = (uint32_t)(((1 << bMax) - 1) << 4);  // column 0 inputs: ~0 / 0 for every block
+    uint32_t wacc = 0;
     D[0] = mq;
     int bCeil = (kb + w - 1) / w;
     if (bCeil < 1) bCeil = 1;
@@ -1086,10 +1096,7 @@ struct BsfLane {
           const int ns = dpBlock(x, carry, vp[r], vn[r]);
           D[r] += ns;
           carry = ns;
-#ifndef GWA_EXP_NOSTORE
-          hvp[((size_t)(j + 1) * bMax + r) * is] = vp[r];
-          hvn[((size_t)(j + 1) * bMax + r) * is] = vn[r];
-#endif
+          hist[((size_t)(j + 1) * bMax + r) * is] = VpVn{vp[r], vn[r]};
           wmask |= 1u << r;
         }
       }
@@ -1106,8 +1113,7 @@ struct BsfLane {
             const uint64_t x = nextPeq;
             const int ns = dpBlock(x, carry, vp[r], vn[r]);
             D[r] = dPrev - carry + ns;
-            hvp[((size_t)(j + 1) * bMax + r) * is] = vp[r];
-            hvn[((size_t)(j + 1) * bMax + r) * is] = vn[r];
+            hist[((size_t)(j + 1) * bMax + r) * is] = VpVn{vp[r], vn[r]};
             wmask |= 1u << r;
           }
         }
@@ -1115,9 +1121,11 @@ struct BsfLane {
       } else {
         while (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
       }
-#ifndef GWA_EXP_NOSTORE
-      wr[(size_t)j * is] = (uint8_t)pend;
-#endif
+      wacc |= pend << (8 * (j & 3));
+      if ((j & 3) == 3) {
+        wr[(size_t)(j >> 2) * is] = wacc;
+        wacc = 0;
+      }
       pend = wmask;
       if (bCeil == bMax) {
         const int dl = pick(D, bCeil - 1);
@@ -1125,85 +1133,83 @@ struct BsfLane {
         if (bestDiff > dl) { bestTail = j; bestDiff = dl; }
       }
     }
-    wr[(size_t)N * is] = (uint8_t)pend;
+    wr[(size_t)(N >> 2) * is] = wacc | (pend << (8 * (N & 3)));
     (void)bestDiff;
     if (!have) return 1;
-    // traceback (:515-643); path chars are appended in reverse order into L.path().  A match decides
-    // the step from the codes alone (:547), so the history is read only at edits.
-    uint8_t *path = L.path();
-    int plen = 0;
+    // Traceback (:515-643).  A match decides the step from the codes alone (:547), so the history is
+    // read only at edits.  The path is generated backwards (CIGAR end first) and run-length encoded
+    // as it goes -- no path array: S/I/D before the first M are the trailing soft clip (`right`),
+    // S/I/D after the last M the leading one (`left`); the runs in between are kept (generation
+    // order) at the top of this read's CIGAR area, CIGAR entry cap-1-i = run i.  The ops then come
+    // out as cigarStr = reverse(path) + CIGAR.add merging would make them (:599-643).
+    uint16_t *cg = L.cigar();
+    const int cap = caps.cigar;
     int row = mq - 1, col = bestTail;
     int diff = 0, leftMostPos = 0;
+    int right = 0, adj = 0;  // trailing S/I/D count, of which I/D
+    int seenM = 0, curT = 0, curL = 0, nRuns = 0, lastM = 0, pendL = 0, pendAdj = 0;
     for (;;) {
-      int pth = 0;  // 0 NONE 1 DIAG 2 DIAG_MM 3 LEFT 4 UP
+      int t = 4, cnt = 1;  // path char of this step: 0 M, 1 I, 2 D, 4 S (cnt of them)
+      int fin = 0;
       if (col >= 0 && row >= 0) {
         if (rc.code(refStart + col, -1) == dpQ(strand, qs, qe, row)) {
-          pth = 1;
+          t = 0;
         } else {
           const int block = row >> 6, offset = row & 63;
-          const uint32_t wb = wr[(size_t)(col + 1) * is];
+          const uint32_t wb = (wr[(size_t)((col + 1) >> 2) * is] >> (8 * ((col + 1) & 3))) & 0xFFu;
           uint64_t vpw = 0, vnw = 0;
           if ((wb >> block) & 1) {  // computed at column col (the later write when both happened)
-            vpw = hvp[((size_t)(col + 1) * bMax + block) * is];
-            vnw = hvn[((size_t)(col + 1) * bMax + block) * is];
+            const VpVn h = hist[((size_t)(col + 1) * bMax + block) * is];
+            vpw = h.vp;
+            vnw = h.vn;
             if ((wb >> (4 + block)) & 1) { vpw = ~0ULL; vnw = 0; }
           } else if ((wb >> (4 + block)) & 1) {
             vpw = ~0ULL;
             vnw = 0;
           }
-          const uint64_t vpf = vpw & (1ULL << offset);
-          const uint64_t vnf = vnw & (1ULL << offset);
-          if (vpf != 0) { pth = 4; diff++; }
-          else if (vnf == 0) { pth = 2; diff++; }
-          else { pth = 3; diff++; }
+          t = (vpw >> offset) & 1 ? 1 : ((vnw >> offset) & 1) == 0 ? 0 : 2;
+          diff++;
+        }
+        if (t == 0) { leftMostPos = col; col--; row--; }
+        else if (t == 1) { leftMostPos = col + 1; row--; }
+        else { col--; }
+      } else {
+        // NONE: the remaining rows become S (:588-597)
+        fin = 1;
+        cnt = row >= 0 ? row + 1 : 0;
+      }
+      if (cnt > 0) {
+        if (!seenM) {
+          if (t == 0) { seenM = 1; curT = 0; curL = 1; lastM = 0; }
+          else { right += cnt; adj += (t == 1 || t == 2) ? 1 : 0; }
+        } else {
+          if (t == curT) {
+            curL += cnt;
+          } else {
+            if (nCigar + 2 * nRuns + 4 > cap) { status = ST_OVERFLOW; return -1; }
+            cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
+            ++nRuns;
+            curT = t;
+            curL = cnt;
+          }
+          if (t == 0) { lastM = nRuns; pendL = 0; pendAdj = 0; }
+          else { pendL += cnt; pendAdj += (t == 1 || t == 2) ? 1 : 0; }
         }
       }
-      if (pth == 1 || pth == 2) { path[plen++ * is] = 'M'; leftMostPos = col; col--; row--; }
-      else if (pth == 4) { path[plen++ * is] = 'I'; leftMostPos = col + 1; row--; }
-      else if (pth == 3) { path[plen++ * is] = 'D'; col--; }
-      else {
-        while (col >= 0 || row >= 0) {
-          if (row >= 0) path[plen++ * is] = 'S';
-          col--;
-          row--;
-        }
-        break;
-      }
+      if (fin) break;
     }
-    // cigarStr = reverse(path); leading/trailing S/I/D -> S, I/D subtract from diff
-    int left = 0, right = 0;
-    for (int i = 0; i < plen; ++i) {
-      const char t = (char)path[(size_t)(plen - 1 - i) * is];
-      if (t == 'S') left++;
-      else if (t == 'I' || t == 'D') { left++; diff--; }
-      else break;
-    }
-    for (int i = plen - 1; i >= left; --i) {
-      const char t = (char)path[(size_t)(plen - 1 - i) * is];
-      if (t == 'S') right++;
-      else if (t == 'I' || t == 'D') { right++; diff--; }
-      else break;
-    }
-    // CIGAR.add(char) over S^left + middle + S^right (A/CIGAR.java:143-156)
     const int off = nCigar;
-    int curT = 4, curL = left;
-    for (int i = left; i < plen - right; ++i) {
-      const char t = (char)path[(size_t)(plen - 1 - i) * is];
-      const int ty = t == 'M' ? 0 : t == 'I' ? 1 : t == 'D' ? 2 : 4;
-      if (ty == curT) { curL++; continue; }
-      if (curL > 0 && putCigarOp(curT, curL) < 0) return -1;
-      curT = ty;
-      curL = 1;
+    if (!seenM) {
+      diff -= adj;  // the whole path is the leading clip (left = plen, right = 0)
+      if (right > 0 && putCigarOp(4, right) < 0) return -1;
+    } else {
+      if (nCigar + 2 * nRuns + 4 > cap) { status = ST_OVERFLOW; return -1; }
+      cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
+      diff -= adj + pendAdj;
+      if (pendL > 0 && putCigarOp(4, pendL) < 0) return -1;
+      for (int i = lastM; i >= 0; --i) cg[nCigar++] = cg[cap - 1 - i];
+      if (right > 0 && putCigarOp(4, right) < 0) return -1;
     }
-    if (right > 0) {
-      if (curT == 4) curL += right;
-      else {
-        if (curL > 0 && putCigarOp(curT, curL) < 0) return -1;
-        curT = 4;
-        curL = right;
-      }
-    }
-    if (curL > 0 && putCigarOp(curT, curL) < 0) return -1;
     *cigOff = off;
     *cigLen = nCigar - off;
     *outPos = leftMostPos;

@@ -63,6 +63,7 @@ def lib():
                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
         L.orc_align_mode.argtypes = L.orc_align.argtypes + [ctypes.c_int]
+        L.orc_align_threads.argtypes = L.orc_align.argtypes + [ctypes.c_int, ctypes.c_int]
         L.orc_free.argtypes = [ctypes.c_void_p]
         L.orc_align_block_detailed.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
@@ -159,8 +160,9 @@ class Index:
                 cur.append((f[0], f[1], int(f[2]), int(f[3]), int(f[4]), int(f[5]), f[6], int(f[7])))
         return out
 
-    def align(self, reads, config=None, with_stats=False, mode=0):
-        """reads: list of (name, seq, qual-or-None). Returns SAM text (no header)."""
+    def align(self, reads, config=None, with_stats=False, mode=0, threads=1):
+        """reads: list of (name, seq, qual-or-None). Returns SAM text (no header).  threads > 1 splits the
+        reads into contiguous ranges aligned on that many host threads (same output, input order)."""
         n = len(reads)
         names = (ctypes.c_char_p * n)(*[r[0].encode() for r in reads])
         seqs = (ctypes.c_char_p * n)(*[r[1].encode() for r in reads])
@@ -169,10 +171,11 @@ class Index:
         out = ctypes.c_void_p()
         ln = ctypes.c_uint64()
         stats = (OrcStats * n)() if with_stats else None
-        rc = lib().orc_align_mode(self.h, ctypes.byref(cfg), n, ctypes.cast(names, ctypes.c_void_p),
-                                  ctypes.cast(seqs, ctypes.c_void_p), ctypes.cast(quals, ctypes.c_void_p),
-                                  ctypes.byref(out), ctypes.byref(ln),
-                                  ctypes.cast(stats, ctypes.c_void_p) if stats is not None else None, mode)
+        rc = lib().orc_align_threads(self.h, ctypes.byref(cfg), n, ctypes.cast(names, ctypes.c_void_p),
+                                     ctypes.cast(seqs, ctypes.c_void_p), ctypes.cast(quals, ctypes.c_void_p),
+                                     ctypes.byref(out), ctypes.byref(ln),
+                                     ctypes.cast(stats, ctypes.c_void_p) if stats is not None else None, mode,
+                                     int(threads))
         if rc != 0:
             raise RuntimeError("oracle align failed: " + _err())
         s = ctypes.string_at(out, ln.value).decode()
