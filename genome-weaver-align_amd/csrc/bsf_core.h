@@ -1004,6 +1004,17 @@ struct BsfLane {
 
   // ---- BitParallelSmithWaterman.alignBlockDetailed (A/BitParallelSmithWaterman.java:141-147,335-644) ----
   // query = q[strand][qs,qe) (reversed for strand 1), ref = T[refStart, refEnd)
+  // refCode through a one-word cache of the 2-bit text and of the N bitmap (the run-ahead's text
+  // walk moves one position per step: one load per 32 / 64 steps)
+  int tcOn = 0;
+  int64_t tcW2 = -1, tcWN = -1;
+  uint64_t tcC2 = 0, tcCN = 0;
+  GWA_HD int refCodeCached(int64_t p) {
+    const int64_t a = p >> 5, b = p >> 6;
+    if (a != tcW2) { tcC2 = ix.text2[a]; tcW2 = a; }
+    if (b != tcWN) { tcCN = ix.textN[b]; tcWN = b; }
+    return ((tcCN >> (p & 63)) & 1) ? 4 : (int)((tcC2 >> ((p & 31) * 2)) & 3);
+  }
   GWA_HD int refCode(int64_t p) const {
     uint64_t nb = ix.textN[p >> 6];
     if ((nb >> (p & 63)) & 1) return 4;
@@ -1411,7 +1422,7 @@ struct BsfLane {
       d.meta |= M_TEXT | (hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD);
       d.lb[0] = (uint32_t)t;
       d.lb[1] = (uint32_t)len;
-      d.lb[2] = (uint32_t)refCode(p);
+      d.lb[2] = (uint32_t)(tcOn ? refCodeCached(p) : refCode(p));
       d.lb[3] = 0;
       for (int i = 0; i < 4; ++i) d.ub[i] = 0;
       d.bBase = 0;
@@ -1685,9 +1696,13 @@ struct BsfLane {
       xT = tt;
       if (ch >= 0) {
         storeStateWord(xC, xCS.state);
-        const int ns = nextStateLocal(xC, xCS, ch);
+        int ns = nextStateLocal(xC, xCS, ch);
         if (ns == -2) return SS_DONE;
         if (ns >= 0) {
+          if (first && xC == xBase) {
+            ns = runAhead(ns);
+            if (ns == -2) return SS_DONE;
+          }
           queueAdd(update(xBase, xC, ns));
           if (first) {
             xMode = 0;
@@ -1747,13 +1762,12 @@ struct BsfLane {
     const int mm = cProcessed(d) + (upper ? cRemaining(d) : 0) - nm;
     return mm * cfg.matchScore - nm * cfg.mismatchPenalty - ns * cfg.splitOpenPenalty;
   }
-  // SearchState.nextState (:840-852) from a register copy of the parent; the child stays cached
-  GWA_HD int nextStateLocal(int c, const DState<R> &cs, int ch) {
+  // SearchState.nextState (:840-852) from a register copy of the parent, into d; false = null
+  GWA_HD bool buildChild(const DState<R> &cs, int ch, DState<R> &d) {
     const int strand = cStrand(cs);
     uint64_t rows[R];
     int nh = 0, nko = 0;
     bool hm = false;
-    DState<R> d;
     d.meta = 0;
     GWA_PT(tf);
     nextSi(cs, ch, d);  // the FM step (next(c, ch)) precedes the automaton (:422-425)
@@ -1763,10 +1777,8 @@ struct BsfLane {
     GWA_PT(tq);
     const bool nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm);
     GWA_PA(PR_NFA, tq);
-    if (!nfaOk) { tr(3, 0, 0, 0); return -1; }
+    if (!nfaOk) { tr(3, 0, 0, 0); return false; }
     tr(4, (uint32_t)nh | ((uint32_t)nko << 8) | ((uint32_t)hm << 16), (uint32_t)rows[0], (uint32_t)(nh > 1 ? rows[1] : 0));
-    int id = allocState();
-    if (id < 0) return -2;
     int nc = cs.cursor, dir = cDir(cs);
     if (dir == D_FORWARD) ++nc;
     else if (dir == D_BACKWARD) --nc;
@@ -1787,12 +1799,110 @@ struct BsfLane {
     d.kOffset = (uint8_t)nko;
 #pragma unroll
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
+    return true;
+  }
+  // the child in a new arena slot (stays cached); -1 null, -2 overflow
+  GWA_HD int nextStateLocal(int c, const DState<R> &cs, int ch) {
+    DState<R> d;
+    if (!buildChild(cs, ch, d)) return -1;
+    int id = allocState();
+    if (id < 0) return -2;
     L.arena()[id] = d;
 #ifndef GWA_NO_CACHE
     cache = d;
     cacheIdx = id;
 #endif
     (void)c;
+    return id;
+  }
+
+  // ---- run-ahead over text-mode match runs ----
+  // When the polled state's first child (its own next base, :386-396) is accepted, the reference
+  // pushes it and ends the iteration; the next poll usually returns that child, whose first child
+  // is tried next, and so on, one FM step per loop iteration.  In text mode (one occurrence) while
+  // the text continues with the read's bases, such a run lasts tens of steps.  If the queue array
+  // provably comes back unchanged from every push + poll of the run (heapNoop: the child sifts up to
+  // the root and the displaced last element sifts back down to its slot), the iterations are run
+  // here back to back in registers: the same FM steps (counted), automaton steps and loop checks
+  // (:352-396) in the same order, without the heap round trips and without arena copies of the
+  // intermediate states, which nothing references (chain-free, not queued, not reported).  The run
+  // stops before any state that the loop would treat otherwise -- report, prune, empty or rejected
+  // first child, non-text interval -- and that state is pushed as the reference pushes it.
+  GWA_HD uint64_t heapKeyAt(int i) const { return L.heap()[(size_t)i * L.hs] >> 16; }
+  GWA_HD bool heapNoop(uint64_t *bound) const {
+    const int kk = heapSize;
+    *bound = ~0ULL;
+    if (kk == 0) return true;
+    const int depth = 31 - __builtin_clz((unsigned)kk + 1u);  // levels above slot kk
+    const uint64_t x = heapKeyAt((kk - 1) >> 1);              // P0's element, displaced to slot kk
+    uint64_t mn = ~0ULL;
+    int ok = 1;
+    for (int j = depth; j >= 1; --j) {
+      const int node = ((kk + 1) >> j) - 1;  // path node, root first; node(1) = P0
+      const uint64_t v = heapKeyAt(node);
+      mn = v < mn ? v : mn;
+      const int lc = 2 * node + 1, rc = lc + 1;
+      if (j >= 2) {
+        // siftDown at node must pick the path child (holding v after the push) and move x below it
+        const int nxt = ((kk + 1) >> (j - 1)) - 1;
+        if (nxt == lc) ok &= (rc < kk && v > heapKeyAt(rc)) ? 0 : 1;
+        else ok &= heapKeyAt(lc) > v ? 1 : 0;
+        ok &= x > v ? 1 : 0;
+      } else if (kk == rc) {
+        ok &= x > heapKeyAt(lc) ? 0 : 1;  // siftDown must stop at P0
+      }
+    }
+    *bound = mn;
+    return ok != 0;
+  }
+  GWA_HD uint64_t keyOfLocal(const DState<R> &c) const {  // keyOf of a chain-free state
+    const int sc = stateScore(c, 0, false);
+    const uint64_t sp = (uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc) & 0xFFFFFFFFULL;
+    return ((uint64_t)(((uint32_t)c.state >> 16) & 0xFF) << 40) | (sp << 8) | (uint64_t)(255 - cProcessed(c));
+  }
+  GWA_HD int runAhead(int ns) {
+#ifdef GWA_NO_RA
+    return ns;
+#endif
+    if (cfg.runAheadMax <= 0 || cacheIdx != ns || cache.nextSplit >= 0 || !siText(cache)) return ns;
+    uint64_t bound;
+    if (!heapNoop(&bound)) return ns;
+    // the run works on the register copy `cache` (the state to be polled next) in place
+    int moved = 0;
+    tcW2 = tcWN = -1;
+    for (int it = 0; it < cfg.runAheadMax; ++it) {
+      // loop top (:352-356) and the poll checks (:358-385) for the cached state
+      if (numFMIndexSearches > upperSearches || status == ST_OVERFLOW || status == ST_ERROR) break;
+      if (keyOfLocal(cache) >= bound) break;
+      if ((((uint32_t)cache.state >> 24) & 3) != 0 || cRemaining(cache) == 0) break;
+      if ((cache.state & 0x1F) == 0x1F) break;
+      const int nm = (int)(((uint32_t)cache.state >> 8) & 0xFF);
+      if (nm > minMismatches) break;
+      const int ubs = stateScore(cache, 0, true);
+      if (ubs < 0 || ubs < bestScore) break;
+      if (!siText(cache)) break;
+      const int nb = qcode(cStrand(cache), cNextIdx(cache));
+      if ((cache.state & (1 << nb)) != 0 || siIsEmpty(cache, nb)) break;
+      // (the parent's checked flag for nb is not recorded: the parent is never read again, and the
+      // child takes only the priority bits of the parent's state word)
+      DState<R> d;
+      const int fm0 = numFMIndexSearches, ts0 = textSteps;
+      tcOn = 1;
+      const bool ok = buildChild(cache, nb, d);
+      tcOn = 0;
+      if (!ok) {  // a rejected first child: the state goes through the loop as the reference runs it
+        numFMIndexSearches = fm0;
+        textSteps = ts0;
+        break;
+      }
+      cache = d;
+      moved = 1;
+    }
+    if (!moved) return ns;
+    const int id = allocState();
+    if (id < 0) return -2;
+    L.arena()[id] = cache;
+    cacheIdx = id;
     return id;
   }
 

@@ -317,6 +317,7 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     sc.indelEndSkip = cfg->indel_end_skip; sc.bandWidth = cfg->band_width;
     sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 16;
     sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
+    sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
     const uint32_t n = reads->n;
     b->n = n;
     b->hasQual = reads->qual != nullptr;

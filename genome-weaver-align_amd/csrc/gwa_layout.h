@@ -76,6 +76,9 @@ struct SearchConfig {
   // 1: search states whose pattern occurs once step by text compares (M_TEXT).  Exact for
   // numSplit <= 1, where no split changes a state's search direction (BsfLane::nextSi)
   int32_t textSearch;
+  // BsfLane::runAhead: at most this many text-mode match steps run back to back per search step
+  // (0 = off).  A lane running ahead holds its wavefront, so long runs cost the other lanes time.
+  int32_t runAheadMax;
 };
 
 // Read batch as resident in HBM: one byte code (0..4) per base; every read starts at a 16-B
