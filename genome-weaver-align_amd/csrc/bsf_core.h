@@ -823,22 +823,81 @@ struct BsfLane {
     return ((tw.cN >> (t & 63)) & 1) ? 4 : (int)((tw.c2 >> ((t & 31) * 2)) & 3);
   }
 
+  // Up to 32 text-mode steps at once: the number of leading matches between the read's bases
+  // q[strand][i, i + L) and the text characters the steps from SA value tp would read
+  // (textBefore(fm, tp), textBefore(fm, tp - 1), ...), compared as 2-bit words (N never matches).
+  // L is capped so the text positions do not wrap around the cyclic text.
+  GWA_HD static uint64_t rev2(uint64_t x) {  // reverse the order of the 32 two-bit fields
+    x = bitrev64(x);
+    return ((x >> 1) & 0x5555555555555555ULL) | ((x & 0x5555555555555555ULL) << 1);
+  }
+  GWA_HD static uint32_t rev32(uint32_t x) {
+#if defined(__clang__)
+    return __builtin_bitreverse32(x);
+#else
+    return (uint32_t)(bitrev64((uint64_t)x) >> 32);
+#endif
+  }
+  // 32 text codes from position s (2-bit fields) and their N flags; positions >= N read as 0
+  GWA_HD void textWin(int64_t s, uint64_t *codes, uint32_t *nb) const {
+    const int64_t last2 = (int64_t)((ix.N - 1) >> 5), lastN = (int64_t)((ix.N - 1) >> 6);
+    const int64_t a = s >> 5, b = s >> 6;
+    const int sa = (int)(s & 31) * 2, sn = (int)(s & 63);
+    const uint64_t a0 = ix.text2[a], a1 = a + 1 <= last2 ? ix.text2[a + 1] : 0ULL;
+    const uint64_t n0 = ix.textN[b], n1 = b + 1 <= lastN ? ix.textN[b + 1] : 0ULL;
+    *codes = sa ? (a0 >> sa) | (a1 << (64 - sa)) : a0;
+    *nb = (uint32_t)(sn ? (n0 >> sn) | (n1 << (64 - sn)) : n0);
+  }
+  GWA_HD int textRun(int fm, uint64_t tp, int strand, int i, int L) {
+    const int64_t N = (int64_t)ix.N;
+    uint64_t tw;
+    uint32_t tn;
+    if (fm) {  // T[N - tp], T[N - tp + 1], ...
+      const int64_t t0 = tp == 0 ? 0 : N - (int64_t)tp;
+      if (L > N - t0) L = (int)(N - t0);
+      textWin(t0, &tw, &tn);
+    } else {   // T[tp - 1], T[tp - 2], ...
+      const int64_t t0 = tp == 0 ? N - 1 : (int64_t)tp - 1;
+      if (L > t0 + 1) L = (int)(t0 + 1);
+      if (t0 >= 31) {
+        textWin(t0 - 31, &tw, &tn);
+        tw = rev2(tw);
+        tn = rev32(tn);
+      } else {
+        textWin(0, &tw, &tn);
+        tw = rev2(tw << (2 * (31 - t0)));
+        tn = rev32(tn << (31 - t0));
+      }
+    }
+    const int w = i >> 5, sh = 2 * (i & 31);
+    const uint64_t qa = strand ? pick(pw1, w) : pick(pw0, w);
+    const uint64_t qb = (w + 1 < QW) ? (strand ? pick(pw1, w + 1) : pick(pw0, w + 1)) : 0ULL;
+    const uint64_t rw = sh ? (qa >> sh) | (qb << (64 - sh)) : qa;
+    const uint64_t x = tw ^ rw;
+    const uint64_t nz = (x | (x >> 1)) & 0x5555555555555555ULL;
+    const int j1 = nz ? __builtin_ctzll(nz) >> 1 : 32;
+    const int j2 = tn ? __builtin_ctz(tn) : 32;
+    const int j = j1 < j2 ? j1 : j2;
+    return j < L ? j : L;
+  }
+
   GWA_HD Scan quickScan(int strand) {
     const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
-    uint64_t lb = 0, ub = ix.N;
+    const uint64_t N = ix.N;
+    uint64_t lb = 0, ub = N;
     int mark = 0, nmm = 0;
     // longestMatch bookkeeping kept branch-free (loop-carried i1 flags in this divergent loop were
     // mis-lowered by the gfx950 backend in our tests); `have` is an int 0/1.
     int have = 0;
     int lmS = 0, lmE = 0;
-    // text mode (textBefore): once the interval is a single row, each further step is one text
-    // character compare; tp = SA value of that row.  uniq is an int 0/1 for the same reason as have.
+    // text mode: once the interval is a single row [lb, lb + 1) with SA value tp, each further step
+    // is one text character compare (textBefore), run 32 at a time by textRun.  uniq is an int 0/1
+    // for the same reason as have.
     int uniq = 0;
     uint64_t tp = 0;
-    TextWalk tw;
-    int i = 0;
     const int K = ix.kmerK;
-    for (; i < m; ++i) {
+    int i = 0;
+    while (i < m) {
       // at a restart from [0, N) (mark == i), the k-mer table answers the next K steps at once
       // when none of them is empty; otherwise the steps below run one by one
       if (K > 0 && i == mark && i + K <= m) {
@@ -850,23 +909,28 @@ struct BsfLane {
           ub = e >> 32;
           quickSteps += K;
           shortSteps += K;
-          i += K - 1;
+          i += K;
           const int u = ub - lb == 1 ? 1 : 0;
           if (u) { tp = ix.sa[fm][lb]; ++saReads; }
           uniq = u;
           continue;
         }
       }
-      int ch = q(strand, i);
-      uint64_t nlb, nub;
+      uint64_t nlb = lb, nub = ub;
+      int empty;
       if (uniq) {
-        const int tc = textBefore(fm, tp, tw);
+        const int L = m - i < 32 ? m - i : 32;
+        const int j = textRun(fm, tp, strand, i, L);
+        tp = tp >= (uint64_t)j ? tp - j : tp + N - j;  // j hits, each moving to SA value tp - 1 (cyclic)
+        i += j;
+        quickSteps += j;
+        shortSteps += j;
+        if (j == L) continue;
+        ++quickSteps;  // the step at i: BWT character != read base, empty interval
         ++shortSteps;
-        const int hit = tc == ch ? 1 : 0;
-        nlb = lb;
-        nub = hit ? ub : lb;
-        tp = hit ? (tp == 0 ? ix.N - 1 : tp - 1) : tp;
+        empty = 1;
       } else {
+        const int ch = q(strand, i);
         // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
         // one 64-B block when lb and ub share a 128-position window
         Block B;
@@ -878,20 +942,21 @@ struct BsfLane {
           ++blocks;
         }
         nub = ix.C[ch] + rankOne(B, ub, ch);
-        if (nub - nlb == 1) { tp = ix.sa[fm][nlb]; ++saReads; uniq = 1; }
+        ++quickSteps;
+        tr(16 + strand, (uint32_t)(i | (ch << 16)), (uint32_t)nlb, (uint32_t)nub);
+        empty = nlb >= nub ? 1 : 0;
+        if (!empty && nub - nlb == 1) { tp = ix.sa[fm][nlb]; ++saReads; uniq = 1; }
       }
-      ++quickSteps;
-      tr(16 + strand, (uint32_t)(i | (ch << 16)), (uint32_t)nlb, (uint32_t)nub);
-      const int empty = nlb >= nub ? 1 : 0;
       const int better = empty & ((have ^ 1) | ((lmE - lmS) < (i - mark) ? 1 : 0));
       lmS = better ? mark : lmS;
       lmE = better ? i : lmE;
       have |= empty;
       nmm += empty;
       lb = empty ? 0 : nlb;
-      ub = empty ? ix.N : nub;
+      ub = empty ? N : nub;
       mark = empty ? i + 1 : mark;
       uniq = empty ? 0 : uniq;
+      ++i;
     }
     {
       const int better = (have ^ 1) | ((lmE - lmS) < (i - mark) ? 1 : 0);

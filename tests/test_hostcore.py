@@ -170,3 +170,27 @@ def test_sf_reads_with_n_and_unmappable(random_genome):
         oi.align([("e0", "", None)], O.OrcConfig.default(k=2.0, strategy=1))
     with pytest.raises(RuntimeError):
         hostcore.HostCore(codes, names, lengths).align([("e0", "", None)], k=2.0, strategy=1)
+
+
+@pytest.mark.parametrize("strategy", [0, 1])
+def test_text_ends_and_word_boundaries(strategy):
+    # reads at the very start / end of the text and straddling contig joins: the text-mode runs
+    # (quick scan and search, 32 bases per compare) meet the text ends and the cyclic wrap there
+    rng = np.random.default_rng(123)
+    lengths = [97, 1500, 2301, 64]
+    codes = rng.integers(0, 4, sum(lengths)).astype(np.uint8)
+    names = ["c%d" % i for i in range(len(lengths))]
+    L = len(codes)
+    reads = []
+    for i, a in enumerate(list(range(0, 40)) + list(range(L - 140, L - 60)) + [95, 1590, 3890, L - 100]):
+        for m in (36, 60, 100):
+            if a + m > L:
+                continue
+            s = codes[a:a + m].copy()
+            for j in rng.integers(0, m, rng.integers(0, 3)):
+                s[j] = (s[j] + rng.integers(1, 4)) % 4
+            if rng.random() < 0.5:
+                s = synth.COMP[s[::-1]]
+            reads.append(("e%d_%d" % (i, m), synth.SYM[s].tobytes().decode(), None))
+    for k in (2.0, 0.1):
+        _cmp(codes, names, lengths, reads, k, strategy=strategy)
