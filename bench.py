@@ -49,7 +49,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--genome", default=os.environ.get("GWA_BENCH_GENOME", "hg19"))
     ap.add_argument("--reads", type=int, default=int(os.environ.get("GWA_BENCH_READS", "0")))
-    ap.add_argument("--k", type=float, default=2.0)
+    ap.add_argument("--k", type=float, default=None, help="max edits (default: 2 for c2, 5 for c4)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4"],
+                    help="c2: 100 bp, 0-2 substitutions (the BASELINE metric); c4: 150 bp, 0-5 edits with indels")
+    ap.add_argument("--strategy", default="bsf", choices=["bsf", "sf"], help="-m (align strategy)")
     ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "20000")),
                     help="reads of the single-thread CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
@@ -59,6 +62,7 @@ def main():
                     help="reads of the multi-core CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=2000, help="reads of step 0 checked against the oracle")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the host-pipeline (FASTQ-to-SAM) leg")
     args = ap.parse_args()
 
     import numpy as np
@@ -84,7 +88,10 @@ def main():
         mb = float(args.genome)
         contigs = [("chr%d" % (i + 1), int(mb * 1e6 / 4)) for i in range(4)]
         gname = "%g Mbp synthetic (4 contigs, i.i.d. ACGT)" % mb
-    reads_per_step = args.reads or (10_000_000 if args.genome == "hg19" else 1_000_000)
+    c4 = args.workload == "c4"
+    if args.k is None:
+        args.k = 5.0 if c4 else 2.0
+    reads_per_step = args.reads or (1_000_000 if c4 else 10_000_000 if args.genome == "hg19" else 1_000_000)
 
     t0 = time.time()
     codes, names, lengths = synth.genome(contigs, config_id=1)
@@ -94,11 +101,13 @@ def main():
     t_index = time.time() - t0
     log("index built + resident in HBM: %.1fs, %.2f GB" % (t_index, gi.deviceBytes() / 1e9))
 
-    cfg = gwa.AlignmentConfig(k=args.k)
-    # synthetic 100 bp reads, 0-2 substitutions, shard = rank
-    m = 100
+    cfg = gwa.AlignmentConfig(k=args.k, strategy=args.strategy)
+    # synthetic reads: C2 100 bp with 0-2 substitutions; C4 150 bp with 0-5 edits,
+    # 60 % substitutions / 20 % 1-bp insertions / 20 % 1-bp deletions; shard = rank
+    m = 150 if c4 else 100
     t0 = time.time()
-    seqs = synth.reads_codes(codes, lengths, reads_per_step, m, 2, config_id=2, shard=rank)
+    seqs = synth.reads_codes(codes, lengths, reads_per_step, m, 2, config_id=4 if c4 else 2, shard=rank,
+                             indels=c4, max_edits=5)
     seq_blob = synth.SYM[seqs].tobytes()
     seq_off = np.arange(0, m * (reads_per_step + 1), m, dtype=np.uint64)
     name_blob, name_off = synth.name_blob(reads_per_step)
@@ -131,6 +140,25 @@ def main():
     barrier()
     dt = gdist.max_over_ranks(time.perf_counter() - t0)
 
+    # host pipeline (first bullet): the whole path for one batch outside the timed
+    # region -- reads from host memory to HBM (batch create), kernels, records back to the host and SAM
+    # text formatted (16 host threads) -- reported beside `value`, never as it
+    pipe = None
+    if rank == 0 and not args.no_pipeline:
+        t0 = time.perf_counter()
+        b2 = gwa.Batch(gi, cfg, blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
+        t1 = time.perf_counter()
+        b2.run()
+        t2 = time.perf_counter()
+        nbytes = b2.sam_size()
+        t3 = time.perf_counter()
+        b2.close()
+        pipe = {"reads_per_s": reads_per_step / (t3 - t0), "h2d_setup_s": t1 - t0, "kernels_s": t2 - t1,
+                "d2h_sam_format_s": t3 - t2, "sam_bytes": nbytes,
+                "note": "one batch, host read blobs -> HBM -> kernels -> host SAM text; index load excluded"}
+        log("host pipeline: %.0f reads/s (setup %.2fs, kernels %.2fs, SAM %.2fs, %.2f GB)"
+            % (pipe["reads_per_s"], t1 - t0, t2 - t1, t3 - t2, nbytes / 1e9))
+
     nres = min(args.check, reads_per_step)
     sam, off = batch.results(0, nres)
     st = batch.stats()
@@ -146,7 +174,7 @@ def main():
         oi = O.Index.from_arrays(codes, names, lengths, sa_f=gi.suffixArray(0), sa_r=gi.suffixArray(1))
         t_oidx = time.time() - t0
         nchk = nres
-        exp = oi.align(reads[:nchk], O.OrcConfig.default(k=args.k))
+        exp = oi.align(reads[:nchk], O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]))
         got = sam
         parity = {"reads": nchk, "identical": got == exp}
         log("parity on %d reads: %s (oracle index %.1fs)" % (nchk, got == exp, t_oidx))
@@ -162,7 +190,7 @@ def main():
             oi = O.Index.from_arrays(codes, names, lengths, sa_f=gi.suffixArray(0), sa_r=gi.suffixArray(1))
         ns = min(args.cpu_sample, len(reads))
         t0 = time.perf_counter()
-        oi.align(reads[:ns], O.OrcConfig.default(k=args.k))
+        oi.align(reads[:ns], O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]))
         ct = time.perf_counter() - t0
         cpu1 = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port",
                 "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the reference "
@@ -173,7 +201,7 @@ def main():
         nt = min(args.cpu_sample_mt, len(reads))
         if T > 1 and nt > 0:
             t0 = time.perf_counter()
-            oi.align(reads[:nt], O.OrcConfig.default(k=args.k), threads=T)
+            oi.align(reads[:nt], O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]), threads=T)
             ct = time.perf_counter() - t0
             cpu = {"value": nt / ct, "unit": "reads/s", "cores": T, "kind": "port",
                    "sample": "first %d reads of rank 0's batch on %d host threads (contiguous ranges, one "
@@ -196,13 +224,14 @@ def main():
     if q_ms >= s_ms:
         dom, ach_bytes, dom_ms, dom_ref = "fm_quickscan", q_bytes, q_ms, q_ref
     else:
-        dom, ach_bytes, dom_ms, dom_ref = "bsf_search", s_bytes, s_ms, s_ref
+        dom, ach_bytes, dom_ms, dom_ref = args.strategy + "_search", s_bytes, s_ms, s_ref
     achieved = ach_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    workload = ("%s; %d x 100 bp reads per GPU per step, 0-2 substitutions, -k %g, -m bsf, besthit"
-                % (gname, reads_per_step, args.k))
+    workload = ("%s; %d x %d bp reads per GPU per step, %s, -k %g, -m %s, besthit"
+                % (gname, reads_per_step, m, "0-5 edits (subs/1-bp indels)" if c4 else "0-2 substitutions", args.k,
+                   args.strategy))
     traffic, traffic_src = _pmc_traffic(dom, workload)
     out = {
-        "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": steps,
+        "metric": METRIC if not c4 else "reads/sec, 150 bp k<=5 with indels vs hg19 (config C4)", "value": value, "unit": "reads/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "config": {"workload": workload,
@@ -218,7 +247,7 @@ def main():
                    "quick_steps_per_read": st.quick_steps / reads_per_step,
                    "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
                    "quick_short_steps_per_read": st.quick_short_steps / reads_per_step,
-                   "cpu_baseline_1thread": cpu1,
+                   "cpu_baseline_1thread": cpu1, "host_pipeline": pipe,
                    "search_short_steps_per_read": st.search_short_steps / reads_per_step,
                    "rank_kernel": {"kernel": "fm_quickscan", "algorithmic_bytes_per_launch": q_bytes,
                                    "ref_equiv_bytes_per_launch": q_ref, "avg_launch_ms": q_ms,

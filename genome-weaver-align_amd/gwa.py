@@ -330,6 +330,15 @@ class Batch:
             _check(lib().gwa_batch_results_range(self.h, first, count, ctypes.byref(res)))
         return _take_results(res)
 
+    def sam_size(self):
+        """Format the whole batch's SAM text in the library (D2H of the records + host formatting) and
+        return its size in bytes without copying it into Python (host-pipeline timing)."""
+        res = _Results()
+        _check(lib().gwa_batch_results(self.h, ctypes.byref(res)))
+        n = res.sam_len
+        lib().gwa_results_free(ctypes.byref(res))
+        return n
+
     def read_counters(self):
         """per read: status, fm_searches, quick_steps, quickscan_blocks, search_blocks, states, sa_reads, n_hits"""
         import numpy as np

@@ -5,7 +5,13 @@
 Per kernel of the align path: dispatch count, average duration (kernel trace), and per-dispatch
 PMC averages.  FETCH_SIZE is rocprofv3's derived memory-side read volume in KiB; per
 /opt/skills/guides/MI355X_MICROARCH.md (§HBM) gfx950 reports half the bytes of 16-B-per-lane
-reads, so `hbm_read_bytes_corrected` = 2 x 1024 x FETCH_SIZE.  Infinity-Cache hits are counted
+reads.  The align kernels do not stream: they gather random 64-B Occ blocks, 8-B words and 4-B
+suffix-array values.  tools/fetch_calib.hip measures FETCH_SIZE on a known count of exactly those
+accesses (profiles/r01_fetch_calibration.json): one random access of 4, 8 or 64 B is tallied as
+64 B per fabric request (x1.00 for 4/8-B words, x1.21 for a 64-B block read as 4 x 16 B), while the
+16-B streaming control reads 1/2 as the guide says.  So `hbm_read_bytes_corrected` = 1 x 1024 x
+FETCH_SIZE (requests x 64 B) for these kernels; `hbm_read_bytes_stream_x2` keeps the guide's
+streaming correction as an upper bound.  Infinity-Cache hits are counted
 in FETCH_SIZE (guide), so this is an upper bound on HBM traffic.
 """
 import csv
@@ -69,7 +75,8 @@ def summarise(d):
     for k, e in res["kernels"].items():
         p = e.get("pmc", {})
         if "FETCH_SIZE" in p:
-            e["hbm_read_bytes_corrected"] = 2.0 * 1024.0 * p["FETCH_SIZE"]
+            e["hbm_read_bytes_corrected"] = 1024.0 * p["FETCH_SIZE"]
+            e["hbm_read_bytes_stream_x2"] = 2.0 * 1024.0 * p["FETCH_SIZE"]
         if "TCC_HIT_sum" in p and "TCC_MISS_sum" in p and p["TCC_HIT_sum"] + p["TCC_MISS_sum"] > 0:
             e["l2_hit_rate"] = p["TCC_HIT_sum"] / (p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
         if "SQ_WAIT_ANY" in p and p.get("SQ_WAVE_CYCLES"):
