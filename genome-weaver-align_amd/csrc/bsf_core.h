@@ -443,9 +443,17 @@ struct BsfLane {
   // a runtime word index is then one ds_read instead of a select chain over registers.
   lds_u64 *qwL = nullptr;
   int qwS = 1;
+  // QueryMask rows P[strand][ch] (A/QueryMask.java:41-67: bit p = (q[strand][p] == ch), p < m) as
+  // PW 64-bit words per row, precomputed once per read into LDS (interleaved like qwL) when the
+  // kernel provides room (pmL != nullptr; m <= 128 kernels); eqWindow is then a two-word funnel
+  // shift instead of a 2-bit compare and two even-bit compresses per NFA step.
+  static constexpr int PW = QW / 2;
+  lds_u64 *pmL = nullptr;
+  int pmS = 1;
 #if !defined(__HIP_DEVICE_COMPILE__)
   uint64_t qwH[2 * QW];
-  GWA_HD void hostWords() { qwL = qwH; qwS = 1; }
+  uint64_t pmH[2 * 4 * PW];
+  GWA_HD void hostWords() { qwL = qwH; qwS = 1; pmL = pmH; pmS = 1; }
 #endif
   GWA_HD int buildMasks() {  // returns the read's N count
 #if !defined(__HIP_DEVICE_COMPILE__)
@@ -457,6 +465,17 @@ struct BsfLane {
     for (int w = 0; w < QW; ++w) {
       qwL[(size_t)w * qwS] = v0[w];
       qwL[(size_t)(QW + w) * qwS] = v1[w];
+    }
+    if (pmL) {
+      lds_u64 *pm = pmL;
+      pmL = nullptr;  // eqWindow computes from the words while the rows are built
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int w = 0; w < PW; ++w) pm[(size_t)((st * 4 + c) * PW + w) * pmS] = eqWindow(st, c, 64 * w);
+      pmL = pm;
     }
     return countN;
   }
@@ -494,6 +513,13 @@ struct BsfLane {
   // bit j = (q[strand][start + j] == ch) for start + j < m, else 0   (start >= 0)
   GWA_HD uint64_t eqWindow(int strand, int ch, int start) const {
     if (start >= m) return 0;
+    if (pmL) {  // from the precomputed rows (bits at positions >= m are 0 there)
+      const int w = start >> 6, sh = start & 63;
+      const size_t row = (size_t)(strand * 4 + ch) * PW;
+      const uint64_t a = (uint64_t)pmL[(row + w) * pmS];
+      const uint64_t b = w + 1 < PW ? (uint64_t)pmL[(row + w + 1) * pmS] : 0ULL;
+      return sh ? (a >> sh) | (b << (64 - sh)) : a;
+    }
     const int w = start >> 5, sh = 2 * (start & 31);
     const uint64_t a = qword(strand, w), b = qword(strand, w + 1), c = qword(strand, w + 2);
     const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a;

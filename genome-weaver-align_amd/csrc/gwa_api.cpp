@@ -96,7 +96,7 @@ struct gwa_batch {
   uint16_t *d_cig = nullptr;
   uint32_t *d_list[2] = {nullptr, nullptr};
   uint32_t *d_all = nullptr;    // -m sf: every read (0..n-1) is searched
-  uint32_t *d_count = nullptr;  // [0] search list, [1..] overflow lists
+  uint32_t *d_count = nullptr;  // [0] search list, [1 + t] overflow list of tier t, [8 + t] tier t work counter
   uint64_t *d_stair = nullptr;
   uint32_t *d_stairBase = nullptr;
   int hitCap = 4, cigCap = 64;
@@ -329,26 +329,53 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
       b->qualOff.assign(reads->qual_off, reads->qual_off + n + 1);
       b->quals.assign(reads->qual + b->qualOff[0], reads->qual + b->qualOff[n]);
     }
-    // codes (ACGTSequence(String): spaces skipped, A/ACGTSequence.java:86-97)
-    b->codes.reserve(b->seqs.size());
+    // codes (ACGTSequence(String): spaces skipped, A/ACGTSequence.java:86-97), each read 16-B
+    // aligned and zero-padded (ReadsView); encoded on up to 16 host threads in two passes (lengths,
+    // then codes at the prefix-summed offsets)
     b->codeOff.resize(n + 1);
+    b->codeLen.resize(n);
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    auto parallel = [&](auto fn) {
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] { fn((uint32_t)((uint64_t)n * t / nt), (uint32_t)((uint64_t)n * (t + 1) / nt)); });
+      for (auto &x : th) x.join();
+    };
+    const char *sq = b->seqs.data();
+    const uint64_t s0 = b->seqOff[0];
+    parallel([&](uint32_t a, uint32_t e) {
+      for (uint32_t i = a; i < e; ++i) {
+        const char *p = sq + (b->seqOff[i] - s0);
+        const uint64_t L = b->seqOff[i + 1] - b->seqOff[i];
+        uint32_t m = 0;
+        for (uint64_t j = 0; j < L; ++j) m += p[j] != ' ';
+        b->codeLen[i] = m;
+      }
+    });
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (tot > 0xFFFFFFFFull) throw std::runtime_error("read batch too large (> 4 GiB of codes)");
+      b->codeOff[i] = (uint32_t)tot;
+      tot += ((uint64_t)b->codeLen[i] + 15) & ~(uint64_t)15;
+    }
+    b->codes.assign(tot + 16, 0);
+    b->codeOff[n] = (uint32_t)(tot + 16);
+    parallel([&](uint32_t a, uint32_t e) {
+      for (uint32_t i = a; i < e; ++i) {
+        const char *p = sq + (b->seqOff[i] - s0);
+        const uint64_t L = b->seqOff[i + 1] - b->seqOff[i];
+        uint8_t *o = b->codes.data() + b->codeOff[i];
+        for (uint64_t j = 0; j < L; ++j)
+          if (p[j] != ' ') *o++ = to3bit((unsigned char)p[j]);
+      }
+    });
     std::vector<int> lens;
     std::vector<char> seen(256, 0);
-    b->codeLen.resize(n);
     for (uint32_t i = 0; i < n; ++i) {
-      b->codeOff[i] = (uint32_t)b->codes.size();
-      for (uint64_t p = b->seqOff[i]; p < b->seqOff[i + 1]; ++p) {
-        char c = b->seqs[p - b->seqOff[0]];
-        if (c != ' ') b->codes.push_back(to3bit((unsigned char)c));
-      }
-      int m = (int)(b->codes.size() - b->codeOff[i]);
-      b->codeLen[i] = (uint32_t)m;
-      b->codes.resize((b->codes.size() + 15) & ~(size_t)15, 0);  // 16-B aligned, zero-padded (ReadsView)
+      const int m = (int)b->codeLen[i];
       b->maxM = std::max(b->maxM, m);
       if (m <= 255 && !seen[(size_t)m]) { seen[(size_t)m] = 1; lens.push_back(m); }
     }
-    b->codes.resize(b->codes.size() + 16, 0);
-    b->codeOff[n] = (uint32_t)b->codes.size();
     // k per length (AlignmentScoreConfig.getMaximumEditDistance)
     for (int m : lens) {
       int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
@@ -387,7 +414,7 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     b->d_cig = devAlloc<uint16_t>((size_t)n * b->cigCap);
     b->d_list[0] = devAlloc<uint32_t>(n);
     b->d_list[1] = devAlloc<uint32_t>(n);
-    b->d_count = devAlloc<uint32_t>(8);
+    b->d_count = devAlloc<uint32_t>(16);
     if (cfg->strategy == 1) {
       std::vector<uint32_t> all(n);
       for (uint32_t i = 0; i < n; ++i) all[i] = i;
@@ -408,14 +435,19 @@ struct Tier {
   int arena, heap, hits, list, cigar, cand;
   uint32_t maxLanes;
 };
-static const Tier kTiers[3] = {
+static const int kNumTiers = 4;
+static const Tier kTiers[kNumTiers] = {
     {256, kLdsHeap, 32, 32, 512, 0, 256u * 1024u},  // heap in LDS
-    {4096, 4096, 256, 256, 4096, 0, 16384u},
+    // every resident lane of the chip (256 CUs x 8 waves x 64) on the next tier: the reads that
+    // outgrow the LDS heap are many at k >= 4 (C4: ~57 % of 150 bp reads at k 5)
+    {1024, 1024, 64, 64, 1024, 0, 128u * 1024u},
+    {4096, 4096, 256, 256, 4096, 0, 32768u},
     {65536, 65536, 4096, 4096, 65536, 0, 1024u},
 };
 // -m sf: no quick-scan exit, every read starts with up to 2 (k + 2) seeds; heap in the slice
-static const Tier kSfTiers[3] = {
+static const Tier kSfTiers[kNumTiers] = {
     {512, 512, 32, 32, 512, 32, 128u * 1024u},
+    {2048, 2048, 64, 64, 2048, 256, 128u * 1024u},
     {8192, 8192, 256, 256, 4096, 1024, 16384u},
     {65536, 65536, 4096, 4096, 65536, 16384, 1024u},
 };
@@ -431,7 +463,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventCreate(&e2));
-    HIPCHK(hipMemsetAsync(b->d_count, 0, 8 * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(b->d_count, 0, 16 * sizeof(uint32_t), s));
     HIPCHK(hipEventRecord(e0, s));
     const bool sf = b->cfg.strategy == 1;
     const char *qtre = sf ? nullptr : getenv("GWA_QTRACE_READ");
@@ -459,7 +491,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     int cur = 0;
     uint32_t n = nSearch;
     const int m = std::max(b->maxM, 1);
-    for (int t = 0; t < 3 && n > 0; ++t) {
+    for (int t = 0; t < kNumTiers && n > 0; ++t) {
       const Tier &T = sf ? kSfTiers[t] : kTiers[t];
       Caps caps;
       caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
@@ -492,7 +524,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
       launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
-                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
+                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
                    (uint32_t *)d_prof, -1);
       {
         std::vector<uint64_t> pv((size_t)lanes * PR_N);
@@ -513,10 +545,10 @@ int gwa_batch_run(gwa_batch_t *b) {
       if (sf)
         launchSfSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv, t == 0 ? b->d_all : b->d_list[cur], n,
                        ix->scratch, stride, caps, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank,
-                       b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s);
+                       b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s);
       else
         launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
-                     b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 4 + t, b->d_list[cur ^ 1], ovfCount, s,
+                     b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
                      traceRead >= 0 ? d_trace : nullptr, traceRead);
 #endif
       if (traceRead >= 0) {

@@ -130,6 +130,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   __shared__ uint64_t qwLds[2 * QW * 256];  // the lanes' 2-bit read words (BsfLane::qword)
   lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
   lane.qwS = 256;
+  // the lanes' QueryMask rows (BsfLane::pmL), m <= 128 only (LDS budget: 2 workgroups per CU)
+  __shared__ uint64_t pmLds[QW == 4 ? 2 * 4 * (QW / 2) * 256 : 1];
+  if (QW == 4) {
+    lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
+    lane.pmS = 256;
+  }
   // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
   // the wavefront runs the parked reports (DP verification + traceback) together once they are at
   // least half of its live lanes, instead of once per lane on a divergent path.
@@ -207,6 +213,11 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
   if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
   lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
   lane.qwS = 256;
+  __shared__ uint64_t pmLds[QW == 4 ? 2 * 4 * (QW / 2) * 256 : 1];
+  if (QW == 4) {
+    lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
+    lane.pmS = 256;
+  }
   for (;;) {
     const uint64_t act = __ballot(1);
     const int lid = __lane_id();

@@ -28,12 +28,13 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
                   int32_t *stats) {
   const int bMax = std::max(1, (maxM + 63) / 64), nref = maxM + 2 * kmax + 2;
   const int dpw = 2 * bMax * (nref + 1), path = maxM + nref + 8, wrn = nref + 2;
-  const Caps tiers[3] = {{256, kLdsHeap, 32, 32, 512, dpw, path, wrn, 0}, {4096, 4096, 256, 256, 4096, dpw, path, wrn, 0},
-                         {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 0}};
+  const Caps tiers[4] = {{256, kLdsHeap, 32, 32, 512, dpw, path, wrn, 0}, {1024, 1024, 64, 64, 1024, dpw, path, wrn, 0},
+                         {4096, 4096, 256, 256, 4096, dpw, path, wrn, 0}, {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 0}};
   // -m sf tiers (gwa_api.cpp kSfTiers)
-  const Caps sfTiers[3] = {{512, 512, 32, 32, 512, dpw, path, wrn, 32}, {8192, 8192, 256, 256, 4096, dpw, path, wrn, 1024},
+  const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, wrn, 32}, {2048, 2048, 64, 64, 2048, dpw, path, wrn, 256},
+                           {8192, 8192, 256, 256, 4096, dpw, path, wrn, 1024},
                            {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 16384}};
-  std::vector<uint8_t> scratch(std::max(laneBytes<R>(tiers[2]), laneBytes<R>(sfTiers[2])) + ilvBytes(tiers[2]) + 4096);
+  std::vector<uint8_t> scratch(std::max(laneBytes<R>(tiers[3]), laneBytes<R>(sfTiers[3])) + ilvBytes(tiers[3]) + 4096);
   const int chains = cfg.reportType == 0 ? 1 : 4;
   const int hitCap = chains * (cfg.numSplit + 1), cigCap = 64 * chains;
   std::vector<OutHit> oh(hitCap);
@@ -48,7 +49,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
     OutHeader hd{};
     std::vector<uint32_t> tv(65537, 0);
     bool traced = false;
-    for (int t = 0; t < 3; ++t) {
+    for (int t = 0; t < 4; ++t) {
       if (strategy == 1) {
         LaneMem<R> L = laneMem<R>(scratch.data(), sfTiers[t]);
         SfLane<R, QW> lane(x->v, cfg, st, L, sfTiers[t]);
