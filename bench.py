@@ -246,6 +246,7 @@ def main():
                    "fm_searches_per_read": st.fm_searches / reads_per_step,
                    "quick_steps_per_read": st.quick_steps / reads_per_step,
                    "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
+                   "tier_ms": [round(x, 3) for x in st.tier_ms],
                    "quick_short_steps_per_read": st.quick_short_steps / reads_per_step,
                    "cpu_baseline_1thread": cpu1, "host_pipeline": pipe,
                    "search_short_steps_per_read": st.search_short_steps / reads_per_step,

@@ -567,6 +567,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipEventElapsedTime(&ms, e1, e2));
       searchMs += ms;
       b->stats.tier_reads[t] = n;
+      b->stats.tier_ms[t] = ms;
       n = nOvf;
       cur ^= 1;
     }

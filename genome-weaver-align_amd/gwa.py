@@ -42,7 +42,7 @@ class BatchStats(ctypes.Structure):
                 ("quick_blocks", ctypes.c_uint64), ("states", ctypes.c_uint64), ("sa_reads", ctypes.c_uint64), ("tier_reads", ctypes.c_uint32 * 4),
                 ("n_mapped", ctypes.c_uint32), ("n_unmapped", ctypes.c_uint32), ("kmer_lookups", ctypes.c_uint64),
                 ("quick_short_steps", ctypes.c_uint64), ("quick_sa_reads", ctypes.c_uint64),
-                ("search_short_steps", ctypes.c_uint64)]
+                ("search_short_steps", ctypes.c_uint64), ("tier_ms", ctypes.c_float * 4)]
 
 
 _lib = None

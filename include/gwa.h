@@ -72,6 +72,7 @@ typedef struct {
   uint64_t quick_short_steps; /* FMQuickScan steps answered without Occ blocks (k-mer table, single-row text compare) */
   uint64_t quick_sa_reads; /* of sa_reads, by fm_quickscan */
   uint64_t search_short_steps; /* search FM steps answered by one text character (single-row states) */
+  float tier_ms[4];        /* search time per capacity tier (HIP events) */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);
