@@ -214,3 +214,28 @@ def test_sf_known_answer_queries_on_gpu(gwa):
     reads = [("exact", "CACTTTAGTATAATTGTTTTTAGTTTTTGGCAAAACTATTGTCTAAACAG", None),
              ("insertion", "CACTTTAGTATAATTGTTTTTAGCCTTTTTGGCAAAACTATTGTCTAAACAG", None)]
     _check(gi, oi, reads, strategy="sf")
+
+
+@pytest.mark.parametrize("strategy", ["bsf", "sf"])
+def test_text_ends_and_word_boundaries_on_gpu(gwa, strategy):
+    # reads at the very start / end of the text and across contig joins, where the 32-base text
+    # compares (quick scan, search run-ahead) meet the text ends and the cyclic wrap
+    rng = np.random.default_rng(123)
+    lengths = [97, 1500, 2301, 64]
+    codes = rng.integers(0, 4, sum(lengths)).astype(np.uint8)
+    names = ["c%d" % i for i in range(len(lengths))]
+    gi, oi = _both(codes, names, lengths)
+    L = len(codes)
+    reads = []
+    for i, a in enumerate(list(range(0, 40)) + list(range(L - 140, L - 60)) + [95, 1590, 3890, L - 100]):
+        for m in (36, 60, 100):
+            if a + m > L:
+                continue
+            s = codes[a:a + m].copy()
+            for j in rng.integers(0, m, rng.integers(0, 3)):
+                s[j] = (s[j] + rng.integers(1, 4)) % 4
+            if rng.random() < 0.5:
+                s = synth.COMP[s[::-1]]
+            reads.append(("e%d_%d" % (i, m), synth.SYM[s].tobytes().decode(), "I" * m))
+    for k in (2.0, 0.1):
+        _check(gi, oi, reads, k=k, strategy=strategy)
