@@ -467,15 +467,30 @@ struct BsfLane {
       qwL[(size_t)(QW + w) * qwS] = v1[w];
     }
     if (pmL) {
-      lds_u64 *pm = pmL;
-      pmL = nullptr;  // eqWindow computes from the words while the rows are built
+      // each 32-base word split once into its two bit planes (code bit 0, code bit 1); the four
+      // rows are then plane combinations (A = 00, C = 01, G = 10, T = 11), A masked to p < m
 #pragma unroll
-      for (int st = 0; st < 2; ++st)
+      for (int st = 0; st < 2; ++st) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int w = 0; w < PW; ++w) {
+          uint64_t rA = 0, rC = 0, rG = 0, rT = 0;
 #pragma unroll
-          for (int w = 0; w < PW; ++w) pm[(size_t)((st * 4 + c) * PW + w) * pmS] = eqWindow(st, c, 64 * w);
-      pmL = pm;
+          for (int h = 0; h < 2; ++h) {
+            const uint64_t v = st ? v1[2 * w + h] : v0[2 * w + h];
+            const uint64_t p0 = compressEven(v), p1 = compressEven(v >> 1);
+            const int valid = m - (64 * w + 32 * h);
+            const uint64_t vm = valid >= 32 ? 0xFFFFFFFFULL : valid <= 0 ? 0ULL : (1ULL << valid) - 1ULL;
+            rA |= (~p0 & ~p1 & vm) << (32 * h);
+            rC |= (p0 & ~p1) << (32 * h);
+            rG |= (~p0 & p1 & 0xFFFFFFFFULL) << (32 * h);
+            rT |= (p0 & p1) << (32 * h);
+          }
+          pmL[(size_t)((st * 4 + 0) * PW + w) * pmS] = rA;
+          pmL[(size_t)((st * 4 + 1) * PW + w) * pmS] = rC;
+          pmL[(size_t)((st * 4 + 2) * PW + w) * pmS] = rG;
+          pmL[(size_t)((st * 4 + 3) * PW + w) * pmS] = rT;
+        }
+      }
     }
     return countN;
   }
@@ -1111,9 +1126,6 @@ struct BsfLane {
     if ((nb >> (p & 63)) & 1) return 4;
     return (int)((ix.text2[p >> 5] >> ((p & 31) * 2)) & 3);
   }
-  // returns 0 ok, 1 null (no alignment), <0 overflow
-  // DP query code p of the fragment q[strand][qs,qe) (reversed on strand 1, :532-534)
-  GWA_HD int dpQ(int strand, int qs, int qe, int p) const { return strand == 1 ? qcode(strand, qe - 1 - p) : qcode(strand, qs + p); }
 
   // One Myers/Hyyro block step (A/BitParallelSmithWaterman.java:476-504); vp/vn in/out
   GWA_HD static int dpBlock(uint64_t x, int hin, uint64_t &vp, uint64_t &vn) {
@@ -1150,6 +1162,7 @@ struct BsfLane {
     }
     return rows >= 64 ? x : (x & ((1ULL << rows) - 1ULL));
   }
+  // returns 0 ok, 1 null (no alignment), <0 overflow
   GWA_HD int alignBlockDetailed(int strand, int qs, int qe, int64_t refStart, int64_t refEnd, int *outPos, int *outDiff,
                                 int *cigOff, int *cigLen) {
     const int w = 64;
@@ -1254,7 +1267,11 @@ struct BsfLane {
       int t = 4, cnt = 1;  // path char of this step: 0 M, 1 I, 2 D, 4 S (cnt of them)
       int fin = 0;
       if (col >= 0 && row >= 0) {
-        if (rc.code(refStart + col, -1) == dpQ(strand, qs, qe, row)) {
+        // query base at row == reference base: the row's bit of Peq[ref base] (no read-word lookup)
+        const int rch = rc.code(refStart + col, -1);
+        const int rb = row >> 6;
+        const uint64_t pq = rch == 0 ? pick(pA, rb) : rch == 1 ? pick(pC, rb) : rch == 2 ? pick(pG, rb) : pick(pT, rb);
+        if (rch < 4 && ((pq >> (row & 63)) & 1ULL)) {
           t = 0;
         } else {
           const int block = row >> 6, offset = row & 63;
@@ -1480,16 +1497,18 @@ struct BsfLane {
     bool hasB = siGetB(c, ch, &bl, &bu);
     if (cDir(c) == D_BIFWD && (int)c.cursor >= (int)c.end - 1) hasF = false;
     const int strand = cStrand(c);
-    uint64_t lo[5], hi[5];
     d.meta = (uint8_t)((d.meta & ~(3 | M_TEXT)) | M_SIVALID);
     // Text mode: the child's pattern P' (P.ch when c's cursor moves forward, ch.P backward; |P'| =
     // processed bases of c + 1) occurs once, either because P does (c in text mode) or because the
     // interval just reached is one row (its SA value gives the occurrence).  The SiSet of P' is then
     // the one text character next to the occurrence in the SiSet's direction.
-    if ((hasF || hasB) && (siText(c) || (cfg.textSearch && (hasF ? fu - fl : bu - bl) == 1))) {
-      const int64_t N = (int64_t)ix.N;
-      int64_t t;
-      int len;
+    enum { K_EMPTY, K_TEXT, K_RANK };
+    const int kind = !(hasF || hasB) ? K_EMPTY
+                     : (siText(c) || (cfg.textSearch && (hasF ? fu - fl : bu - bl) == 1)) ? K_TEXT : K_RANK;
+    const int64_t N = (int64_t)ix.N;
+    int64_t t = 0, p = 0;
+    int len = 0;
+    if (kind == K_TEXT) {
       if (siText(c)) {
         len = (int)c.lb[1] + 1;
         t = (int64_t)c.lb[0];
@@ -1507,39 +1526,49 @@ struct BsfLane {
       // the next character: after the occurrence for a forward SiSet on strand 0 / a backward one
       // on strand 1, before it otherwise
       const bool after = (strand == 0) == hasF;
-      int64_t p = after ? t + len : t - 1;
+      p = after ? t + len : t - 1;
       p = p >= N ? p - N : p < 0 ? p + N : p;
+    }
+    // The memory reads of this FM step -- the text words (text mode) or the two Occ blocks of the
+    // interval (rankACGTN at lb and ub, A/FMIndexOnOccTable.java:53-55; shared when both fall in one
+    // 128-position window) -- are issued for all lanes of the wavefront before any is used, so a
+    // wavefront mixing text-mode and Occ lanes waits once, not once per kind.
+    const int fmR = hasF ? (strand == 0 ? 1 : 0) : (strand == 0 ? 0 : 1);
+    uint64_t rl = hasF ? fl : bl, ru = hasF ? fu : bu;
+    rl = rl > ix.N ? ix.N : rl;
+    ru = ru > ix.N ? ix.N : ru;
+    uint64_t w2 = 0, wN = 0;
+    Block B0, B1;
+    if (kind == K_TEXT && !tcOn) {
+      w2 = ix.text2[p >> 5];
+      wN = ix.textN[p >> 6];
+    }
+    if (kind == K_RANK) {
+      loadBlock(ix.occ[fmR], rl >> 7, B0);
+      loadBlock(ix.occ[fmR], ru >> 7, B1);  // same line when both share a window (an L2 hit)
+      blocks += 1 + ((ru >> 7) != (rl >> 7) ? 1 : 0);
+    }
+    if (kind == K_TEXT) {
       ++textSteps;
       d.meta |= M_TEXT | (hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD);
       d.lb[0] = (uint32_t)t;
       d.lb[1] = (uint32_t)len;
-      d.lb[2] = (uint32_t)(tcOn ? refCodeCached(p) : refCode(p));
+      d.lb[2] = (uint32_t)(tcOn ? refCodeCached(p) : ((wN >> (p & 63)) & 1) ? 4 : (int)((w2 >> ((p & 31) * 2)) & 3));
       d.lb[3] = 0;
       for (int i = 0; i < 4; ++i) d.ub[i] = 0;
       d.bBase = 0;
       return;
     }
-    if (hasF) {
-      const int fm = strand == 0 ? 1 : 0;
-      rank2(fm, fl, fu, lo, hi);
+    if (kind == K_RANK) {
+      uint64_t lo[5], hi[5];
+      rankAll(B0, rl, lo);
+      rankAll(B1, ru, hi);
       for (int i = 0; i < 4; ++i) {
         d.lb[i] = (uint32_t)(ix.C[i] + lo[i]);
         d.ub[i] = (uint32_t)(ix.C[i] + hi[i]);
       }
-      if (!hasB) { d.meta |= SI_FWD; d.bBase = 0; return; }
-      d.meta |= SI_BID;
-      d.bBase = bl;
-      return;
-    }
-    if (hasB) {
-      const int fm = strand == 0 ? 0 : 1;
-      rank2(fm, bl, bu, lo, hi);
-      for (int i = 0; i < 4; ++i) {
-        d.lb[i] = (uint32_t)(ix.C[i] + lo[i]);
-        d.ub[i] = (uint32_t)(ix.C[i] + hi[i]);
-      }
-      d.meta |= SI_BWD;
-      d.bBase = 0;
+      d.meta |= hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD;
+      d.bBase = hasF && hasB ? bl : 0;
       return;
     }
     d.meta |= SI_EMPTY;
