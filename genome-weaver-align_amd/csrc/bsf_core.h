@@ -1491,7 +1491,10 @@ struct BsfLane {
 
   // Cursor.nextSi + FMIndexOnGenome.bidirectionalSearch (S/Cursor.java:182-196, A/FMIndexOnGenome.java:162-191)
   // writes the resulting SiSet into d (lb/ub/bBase/meta-type)
-  GWA_HD void nextSi(const DState<R> &c, int ch, DState<R> &d) {
+  // `between` runs after the FM step's reads are issued and before their values are used: the
+  // caller puts independent work there (the automaton step), so it overlaps the read latency
+  template <class F>
+  GWA_HD void nextSi(const DState<R> &c, int ch, DState<R> &d, F &&between) {
     uint32_t fl = 0, fu = 0, bl = 0, bu = 0;
     bool hasF = siGetF(c, ch, &fl, &fu);
     bool hasB = siGetB(c, ch, &bl, &bu);
@@ -1548,6 +1551,7 @@ struct BsfLane {
       loadBlock(ix.occ[fmR], ru >> 7, B1);  // same line when both share a window (an L2 hit)
       blocks += 1 + ((ru >> 7) != (rl >> 7) ? 1 : 0);
     }
+    between();
     if (kind == K_TEXT) {
       ++textSteps;
       d.meta |= M_TEXT | (hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD);
@@ -1889,14 +1893,15 @@ struct BsfLane {
     int nh = 0, nko = 0;
     bool hm = false;
     d.meta = 0;
+    // The FM step (next(c, ch)) precedes the automaton in the reference (:422-425); the two are
+    // independent (both read only the parent), so the automaton step runs while the FM step's
+    // reads are in flight.  Counts and results are those of the reference order.
+    bool nfaOk = false;
     GWA_PT(tf);
-    nextSi(cs, ch, d);  // the FM step (next(c, ch)) precedes the automaton (:422-425)
+    nextSi(cs, ch, d, [&] { nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm); });
     GWA_PA(PR_FM, tf);
     ++numFMIndexSearches;
     tr(2, (uint32_t)ch, d.lb[0] ^ (d.ub[1] * 3u) ^ (d.lb[2] * 7u) ^ (d.ub[3] * 11u) ^ d.bBase, (uint32_t)(d.meta & 3));
-    GWA_PT(tq);
-    const bool nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm);
-    GWA_PA(PR_NFA, tq);
     if (!nfaOk) { tr(3, 0, 0, 0); return false; }
     tr(4, (uint32_t)nh | ((uint32_t)nko << 8) | ((uint32_t)hm << 16), (uint32_t)rows[0], (uint32_t)(nh > 1 ? rows[1] : 0));
     int nc = cs.cursor, dir = cDir(cs);
