@@ -192,9 +192,16 @@ def main():
         t0 = time.perf_counter()
         oi.align(reads[:ns], O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]))
         ct = time.perf_counter() - t0
+        model = "unknown CPU"
+        try:
+            with open("/proc/cpuinfo") as f:
+                model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), model)
+        except OSError:
+            pass
         cpu1 = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port",
                 "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the reference "
-                          "BSF path (oracle/), same index" % ns}
+                          "%s path (oracle/; CPU restatement, not the JVM), same index; %s"
+                          % (ns, args.strategy.upper(), model)}
         log("cpu baseline (1 thread): %.0f reads/s (%d reads in %.1fs)" % (ns / ct, ns, ct))
         cpu = cpu1
         T = max(1, args.cpu_threads)
@@ -205,8 +212,8 @@ def main():
             ct = time.perf_counter() - t0
             cpu = {"value": nt / ct, "unit": "reads/s", "cores": T, "kind": "port",
                    "sample": "first %d reads of rank 0's batch on %d host threads (contiguous ranges, one "
-                             "Aligner each), C++ restatement of the reference BSF path (oracle/), same index"
-                             % (nt, T)}
+                             "Aligner each), C++ restatement of the reference %s path (oracle/; CPU "
+                             "restatement, not the JVM), same index; %s" % (nt, T, args.strategy.upper(), model)}
             log("cpu baseline (%d threads): %.0f reads/s (%d reads in %.1fs)" % (T, nt / ct, nt, ct))
 
     # roofline of the dominant kernel.  Algorithmic bytes = the bytes this path's algorithm must read
