@@ -58,6 +58,9 @@ int fail(const std::string &m) {
 
 }  // namespace
 
+// error path shared with reads_io.cpp (sets gwa_last_error)
+extern "C" int gwa_fail_message(const char *msg) { return fail(msg); }
+
 struct gwa_index {
   int device = 0;
   hipStream_t stream = nullptr;

@@ -31,6 +31,10 @@ class _Reads(ctypes.Structure):
                 ("name_off", ctypes.c_void_p), ("seq_off", ctypes.c_void_p), ("qual_off", ctypes.c_void_p)]
 
 
+class _ReadBuf(ctypes.Structure):
+    _fields_ = [("reads", _Reads), ("priv", ctypes.c_void_p)]
+
+
 class _Results(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_uint32), ("sam", ctypes.c_void_p), ("sam_len", ctypes.c_uint64),
                 ("line_off", ctypes.c_void_p)]
@@ -52,7 +56,7 @@ EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_inde
            "gwa_index_build_codes", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
            "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
            "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
-           "gwa_batch_read_counters", "gwa_batch_results_range"]
+           "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_reads_parse", "gwa_reads_free"]
 
 
 def lib():
@@ -84,6 +88,8 @@ def lib():
         L.gwa_batch_free.argtypes = [V]
         L.gwa_batch_read_counters.argtypes = [V, V]
         L.gwa_batch_results_range.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, P(_Results)]
+        L.gwa_reads_parse.argtypes = [ctypes.c_char_p, U64, I, I, P(_ReadBuf), P(U64)]
+        L.gwa_reads_free.argtypes = [P(_ReadBuf)]
         _lib = L
     return _lib
 
@@ -264,6 +270,68 @@ class BidirectionalSuffixFilter:
         """Aligner.align(Read, Reporter): reporter(line) once per emitted SAM line."""
         for line in self.align_batch([read]).splitlines():
             reporter(line)
+
+
+class ParsedReads:
+    """Reads parsed from FASTA / FASTQ text by the library (gwa_reads_parse): the records of a text
+    chunk as a gwa_reads_t over library-owned blobs.  consumed = bytes of the chunk parsed (the
+    rest starts an unfinished record unless final)."""
+
+    def __init__(self, text, fmt, final=True):
+        self._buf = _ReadBuf()
+        self._text = bytes(text)
+        used = ctypes.c_uint64()
+        _check(lib().gwa_reads_parse(self._text, len(self._text), {"fasta": 0, "fastq": 1}[fmt], 1 if final else 0,
+                                     ctypes.byref(self._buf), ctypes.byref(used)))
+        self.consumed = used.value
+        self.n = self._buf.reads.n
+
+    def slice(self, first, count):
+        """A gwa_reads_t for reads [first, first + count) (offsets stay absolute)."""
+        r0 = self._buf.reads
+        r = _Reads()
+        r.n = count
+        r.name, r.seq, r.qual = r0.name, r0.seq, r0.qual
+        r.name_off = r0.name_off + 8 * first
+        r.seq_off = r0.seq_off + 8 * first
+        r.qual_off = (r0.qual_off + 8 * first) if r0.qual_off else None
+        return r
+
+    def records(self):
+        """[(name, seq, qual-or-None)] (tests)."""
+        import numpy as np
+        r = self._buf.reads
+        out = []
+        if r.n == 0:
+            return out
+        offs = [np.ctypeslib.as_array((ctypes.c_uint64 * (r.n + 1)).from_address(a)) if a else None
+                for a in (r.name_off, r.seq_off, r.qual_off)]
+        blobs = [ctypes.string_at(p, int(o[-1])) if o is not None else None
+                 for p, o in zip((r.name, r.seq, r.qual), offs)]
+        for i in range(r.n):
+            f = [b[o[i]:o[i + 1]].decode() if o is not None else None for b, o in zip(blobs, offs)]
+            out.append((f[0], f[1], f[2]))
+        return out
+
+    def close(self):
+        if self._buf.priv:
+            lib().gwa_reads_free(ctypes.byref(self._buf))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def align_reads(aligner_, reads_struct):
+    """SAM text of a gwa_reads_t (ParsedReads.slice) through aligner_'s index and config."""
+    res = _Results()
+    c = aligner_.config._c()
+    _check(lib().gwa_align_batch(aligner_.fmIndex.h, ctypes.byref(c), ctypes.byref(reads_struct), ctypes.byref(res)))
+    s = ctypes.string_at(res.sam, res.sam_len).decode() if res.sam_len else ""
+    lib().gwa_results_free(ctypes.byref(res))
+    return s
 
 
 class SuffixFilter(BidirectionalSuffixFilter):

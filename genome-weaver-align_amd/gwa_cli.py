@@ -19,6 +19,7 @@ import argparse
 import gzip
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -83,29 +84,25 @@ def reads_of(path):
         f.close()
 
 
-def _batches(it, n):
-    buf = []
-    for r in it:
-        buf.append(r)
-        if len(buf) >= n:
-            yield buf
-            buf = []
-    if buf:
-        yield buf
-
-
-def _homogeneous(batch):
-    """A device batch carries qualities for every read or for none: split mixed runs."""
-    cur, has = [], None
-    for r in batch:
-        h = r[2] is not None
-        if cur and h != has:
-            yield cur
-            cur = []
-        cur.append(r)
-        has = h
-    if cur:
-        yield cur
+def native_chunks(path, chunk=64 << 20):
+    """The read file as library-parsed chunks (gwa.ParsedReads, include/gwa.h gwa_reads_parse): the
+    host side of the pipeline stays native for large files; read_fasta / read_fastq state the same
+    record rules in Python (tests/test_cli.py holds the two to identical output)."""
+    kind = _kind(path)
+    opener = gzip.open if path.endswith(".gz") else open
+    with opener(path, "rb") as f:
+        carry = b""
+        while True:
+            data = f.read(chunk)
+            final = not data
+            buf = carry + data
+            if not buf:
+                return
+            pr = gwa.ParsedReads(buf, kind, final)
+            yield pr
+            carry = buf[pr.consumed:]
+            if final:
+                return
 
 
 def build_parser():
@@ -133,6 +130,7 @@ def build_parser():
     a.add_argument("-W", dest="bandWidth", type=int, default=31)
     a.add_argument("--device", type=int, default=0, help="GPU ordinal")
     a.add_argument("--batch", type=int, default=1 << 20, help="reads per device batch")
+    a.add_argument("--timing", action="store_true", help="index / align wall times and reads/s on stderr")
     return ap
 
 
@@ -153,17 +151,30 @@ def align(ns, out=sys.stdout):
     if ns.query is None and len(ns.readFiles) != 1:
         raise gwa.GwaError("# of input read files must be one (single-end)")
     cfg = config_of(ns)
+    if ns.query is None:
+        _kind(ns.readFiles[0])  # unsupported suffixes fail before the index is built
+    t0 = time.perf_counter()
     fm = gwa.FMIndexOnGenome.load(ns.refSeq, device=ns.device)
+    t1 = time.perf_counter()
     bsf = gwa.aligner(fm, cfg)
     w = (lambda s: None) if ns.silent else out.write
     w(fm.samHeader())
-    src = iter([("read", ns.query, None)]) if ns.query is not None else reads_of(ns.readFiles[0])
     n = 0
-    for batch in _batches(src, ns.batch):
-        for part in _homogeneous(batch):
-            w(bsf.align_batch(part))
-            n += len(part)
+    if ns.query is not None:
+        w(bsf.align_batch([("read", ns.query, None)]))
+        n = 1
+    else:
+        for pr in native_chunks(ns.readFiles[0]):
+            for i in range(0, pr.n, ns.batch):
+                c = min(ns.batch, pr.n - i)
+                w(gwa.align_reads(bsf, pr.slice(i, c)))
+                n += c
+            pr.close()
+    t2 = time.perf_counter()
     fm.close()
+    if ns.timing:
+        print("[gwa] index load %.2fs; align (read file -> SAM, index load excluded) %.2fs: %.0f reads/s"
+              % (t1 - t0, t2 - t1, n / max(t2 - t1, 1e-9)), file=sys.stderr)
     return n
 
 

@@ -46,6 +46,14 @@ typedef struct {
   const uint64_t *name_off, *seq_off, *qual_off;
 } gwa_reads_t;
 
+/* Reads parsed by the library from FASTA / FASTQ text (gwa_reads_parse); `reads` points into
+ * library-owned blobs until gwa_reads_free.  Replaces the reference's read-file readers
+ * (R/ReadReaderFactory.java:126-151, utgb FastqReader: unvendored, record rules in reads_io.cpp). */
+typedef struct {
+  gwa_reads_t reads;
+  void *priv;
+} gwa_read_buf_t;
+
 /* Library-owned SAM text (no header), in input order; read i's lines are
  * sam[line_off[i], line_off[i+1]).  Free with gwa_results_free. */
 typedef struct {
@@ -98,6 +106,12 @@ void gwa_index_close(gwa_index_t *ix);
 int gwa_align_batch(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_results_t *out);
 void gwa_results_free(gwa_results_t *r);
 void gwa_free(void *p);
+
+/* Parse the complete records of text[0, len): format 0 = FASTA, 1 = FASTQ.  With final = 0 the
+ * last record may continue past len and is left for the next call; *consumed = bytes parsed
+ * (the caller keeps text[*consumed, len) in front of its next chunk).  <0 on a malformed record. */
+int gwa_reads_parse(const char *text, uint64_t len, int format, int final, gwa_read_buf_t *out, uint64_t *consumed);
+void gwa_reads_free(gwa_read_buf_t *b);
 
 /* Split form used by bench.py: upload once (reads resident in HBM), run the kernels (timed),
  * then fetch results. */

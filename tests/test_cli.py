@@ -56,10 +56,61 @@ def test_options_and_errors():
         gwa_cli.align(ns, out=io.StringIO())
 
 
-def test_batches_split_mixed_quality():
-    b = [("a", "A", None), ("b", "C", "I"), ("c", "G", "I"), ("d", "T", None)]
-    assert [len(p) for p in gwa_cli._homogeneous(b)] == [1, 2, 1]
-    assert [len(x) for x in gwa_cli._batches(iter(range(5)), 2)] == [2, 2, 1]
+def _py_records(text, fmt):
+    f = io.StringIO(text.decode(), newline=None)  # text mode: universal newlines, as _open
+    return list(gwa_cli.read_fasta(f) if fmt == "fasta" else gwa_cli.read_fastq(f))
+
+
+def _native_records(text, fmt, chunk):
+    # the CLI's chunked native parse (gwa_reads_parse with the unparsed tail carried over)
+    out, carry, pos = [], b"", 0
+    while True:
+        data = text[pos:pos + chunk]
+        pos += len(data)
+        final = not data
+        buf = carry + data
+        if not buf:
+            return out
+        pr = gwa.ParsedReads(buf, fmt, final)
+        out += pr.records()
+        carry = buf[pr.consumed:]
+        pr.close()
+        if final:
+            return out
+
+
+FASTA_CASES = [b">r1 desc\nACGT\n  AC GT \r\n>r2\r\nNNNN\r>  \nAC\n", b"junk\n>a\n\nAC\n\n>b x y\nG", b"",
+               b">only\n", b">\t t\x0bz\nac\x1cgt\n\n", b"no header\nat all\n"]
+FASTQ_CASES = [b"@a x\nACGT\n+\nIIII\n\n@b\r\nAC\r\n+b\r\nII\r\n", b"\n\n@r\nA\n+\nI", b"",
+               b"@\tq1\x0c extra\nACGN\n+q1\n!!!!\n@q2\n\n+\n\n"]
+
+
+@pytest.mark.parametrize("i", range(len(FASTA_CASES)))
+def test_native_fasta_parser_matches_python(i):
+    t = FASTA_CASES[i]
+    exp = _py_records(t, "fasta")
+    for chunk in range(1, len(t) + 2):
+        assert _native_records(t, "fasta", chunk) == exp, chunk
+
+
+@pytest.mark.parametrize("i", range(len(FASTQ_CASES)))
+def test_native_fastq_parser_matches_python(i):
+    t = FASTQ_CASES[i]
+    exp = _py_records(t, "fastq")
+    for chunk in range(1, len(t) + 2):
+        assert _native_records(t, "fastq", chunk) == exp, chunk
+
+
+def test_native_parser_fixtures_and_errors():
+    for name, fmt in (("sample.fastq", "fastq"), ("test2.fa", "fasta")):
+        t = open(os.path.join(HERE, "golden", "fixtures", name), "rb").read()
+        assert _native_records(t, fmt, 1 << 20) == _py_records(t, fmt)
+        assert _native_records(t, fmt, 7) == _py_records(t, fmt)
+    for bad in (b"@a\nAC\n+\nI\n", b"x\nAC\n+\nII\n", b"@a\nAC\n-\nII\n", b"@a\nAC\n"):
+        with pytest.raises(gwa.GwaError):
+            gwa.ParsedReads(bad, "fastq", True)
+        with pytest.raises(gwa.GwaError):
+            _py_records(bad, "fastq")
 
 
 @pytest.mark.gpu
