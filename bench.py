@@ -26,11 +26,13 @@ def log(*a):
 
 def _pmc_traffic(kernel, workload):
     """Per-launch HBM read bytes of `kernel` from the newest committed rocprofv3 PMC summary of the
-    same workload (profiles/*_profile.json, written by tools/prof_summary.py from FETCH_SIZE with
-    the guide's gfx950 x2 correction); (None, None) when no profile of this workload exists."""
+    same workload (profiles/*_profile.json, written by tools/prof_summary.py from FETCH_SIZE, see
+    profiles/README.md for the correction); (None, None) when no profile of this workload exists.
+    "Newest" is by round tag in the file name (r01 < r01c < r01d ...): file mtimes do not survive a
+    checkout."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_profile.json")), key=os.path.getmtime):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_profile.json")), key=os.path.basename):
         try:
             d = json.load(open(f))
             line = d.get("bench_lines", {}).get("bench.json", {})
