@@ -4,7 +4,11 @@ One step = one pass of the hot path (fm_quickscan + bsf_search tiers) over one b
 100 bp reads already resident in HBM.  Weak scaling: every rank holds a full index replica on its
 own GPU and aligns its own shard; value = total reads of all ranks / max-over-ranks time.
 
-  python bench.py [--gpus N --steps K --warmup W] [--genome hg19|ecoli|<Mbp>] [--reads R]
+  python bench.py [--gpus N --steps K --warmup W] [--genome hg19|hg19r|ecoli|<Mbp>] [--reads R]
+
+--gpus N > 1 without a torch.distributed environment re-launches this script under
+`torch.distributed.run` with N ranks (before anything touches the GPU); ranks beyond the visible GPU
+count share GPUs round-robin (each rank keeps its own index replica).
 """
 import argparse
 import json
@@ -44,28 +48,75 @@ def _pmc_traffic(kernel, workload):
     return best if best else (None, None)
 
 
+def host_cores():
+    """(cores this process may use, description): the CPU affinity set, capped by a cgroup v2 CPU
+    quota when one is set (a GPU box grants each job a share of the host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return n, "affinity %d CPUs, cgroup quota %s" % (aff, "none" if quota is None else "%.1f CPUs" % quota)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "unknown CPU")
+    except OSError:
+        return "unknown CPU"
+
+
+def spawn_ranks(args):
+    """--gpus N outside torch.distributed: run N ranks of this script under torch.distributed.run and
+    exit with its status (this process never initialises the GPU)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--genome", default=os.environ.get("GWA_BENCH_GENOME", "hg19"))
+    ap.add_argument("--genome", default=os.environ.get("GWA_BENCH_GENOME", "hg19"),
+                    help="hg19: hg19 contig lengths, i.i.d. ACGT (the BASELINE config); hg19r: hg19-like "
+                         "repeats and N gaps (tools/synth.genome_repeats); ecoli; or a size in Mbp")
     ap.add_argument("--reads", type=int, default=int(os.environ.get("GWA_BENCH_READS", "0")))
     ap.add_argument("--k", type=float, default=None, help="max edits (default: 2 for c2, 5 for c4)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c4"],
                     help="c2: 100 bp, 0-2 substitutions (the BASELINE metric); c4: 150 bp, 0-5 edits with indels")
     ap.add_argument("--strategy", default="bsf", choices=["bsf", "sf"], help="-m (align strategy)")
-    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "20000")),
-                    help="reads of the single-thread CPU baseline")
-    ap.add_argument("--cpu-threads", type=int, default=min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-                                                           or (os.cpu_count() or 1)),
-                    help="host threads of the multi-core CPU baseline (SURVEY.md 8(d)(ii))")
-    ap.add_argument("--cpu-sample-mt", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE_MT", "160000")),
-                    help="reads of the multi-core CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "100000")),
+                    help="reads of the single-thread CPU baseline (SURVEY.md 8(d)(i))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the multi-core CPU baseline (default: the cores this process may use)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target duration of the multi-core CPU baseline (sample sized from the 1-thread rate)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--check", type=int, default=2000, help="reads of step 0 checked against the oracle")
+    ap.add_argument("--check", type=int, default=20000,
+                    help="random reads of step 0 checked against the oracle (plus every read a search tier >= 1 ran)")
+    ap.add_argument("--sa-check", type=int, default=1 << 20,
+                    help="adjacent suffix-array pairs checked independently (plus a permutation check)")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the host-pipeline (FASTQ-to-SAM) leg")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
 
     import numpy as np
     import synth
@@ -73,33 +124,38 @@ def main():
     import dist as gdist
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     if dist:
         import torch.distributed as tdist
         tdist.init_process_group("gloo")
     import torch
-    torch.cuda.set_device(local)
+    dev = gdist.device_for(local, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
 
-    if args.genome == "hg19":
-        contigs, gname = synth.HG19_CONTIGS, "hg19-size synthetic (i.i.d. ACGT, hg19 contig lengths)"
+    t0 = time.time()
+    if args.genome in ("hg19", "hg19r"):
+        if args.genome == "hg19":
+            codes, names, lengths = synth.genome(synth.HG19_CONTIGS, config_id=1)
+            gname = "hg19-size synthetic (i.i.d. ACGT, hg19 contig lengths)"
+        else:
+            codes, names, lengths = synth.genome_repeats(synth.HG19_CONTIGS, config_id=1)
+            gname = ("hg19-like synthetic (hg19 contig lengths, N gaps, interspersed repeat families, satellites, "
+                     "segmental duplications; tools/synth.genome_repeats)")
     elif args.genome == "ecoli":
-        contigs, gname = synth.ECOLI, "E. coli-size synthetic (4,641,652 bp i.i.d. ACGT)"
+        codes, names, lengths = synth.genome(synth.ECOLI, config_id=1)
+        gname = "E. coli-size synthetic (4,641,652 bp i.i.d. ACGT)"
     else:
         mb = float(args.genome)
-        contigs = [("chr%d" % (i + 1), int(mb * 1e6 / 4)) for i in range(4)]
+        codes, names, lengths = synth.genome([("chr%d" % (i + 1), int(mb * 1e6 / 4)) for i in range(4)], config_id=1)
         gname = "%g Mbp synthetic (4 contigs, i.i.d. ACGT)" % mb
     c4 = args.workload == "c4"
     if args.k is None:
         args.k = 5.0 if c4 else 2.0
-    reads_per_step = args.reads or (1_000_000 if c4 else 10_000_000 if args.genome == "hg19" else 1_000_000)
-
+    reads_per_step = args.reads or (1_000_000 if c4 else 10_000_000 if args.genome.startswith("hg19") else 1_000_000)
+    log("rank %d/%d on GPU %d: genome %d bp generated in %.1fs" % (rank, world, dev, len(codes), time.time() - t0))
     t0 = time.time()
-    codes, names, lengths = synth.genome(contigs, config_id=1)
-    log("genome %d bp generated in %.1fs" % (len(codes), time.time() - t0))
-    t0 = time.time()
-    gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths, device=local)
+    gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths, device=dev)
     t_index = time.time() - t0
     log("index built + resident in HBM: %.1fs, %.2f GB" % (t_index, gi.deviceBytes() / 1e9))
 
@@ -111,6 +167,7 @@ def main():
     seqs = synth.reads_codes(codes, lengths, reads_per_step, m, 2, config_id=4 if c4 else 2, shard=rank,
                              indels=c4, max_edits=5)
     seq_blob = synth.SYM[seqs].tobytes()
+    del seqs
     seq_off = np.arange(0, m * (reads_per_step + 1), m, dtype=np.uint64)
     name_blob, name_off = synth.name_blob(reads_per_step)
     qual_blob = b"I" * (m * reads_per_step)
@@ -118,8 +175,9 @@ def main():
     t0 = time.time()
     batch = gwa.Batch(gi, cfg, blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
     log("batch resident in HBM: %.1fs" % (time.time() - t0))
-    nchk = min(max(args.check, max(args.cpu_sample, args.cpu_sample_mt) if not args.no_cpu else 0), reads_per_step)
-    reads = [(name_blob[10 * i:10 * i + 10].decode(), seq_blob[m * i:m * i + m].decode(), "I" * m) for i in range(nchk)]
+
+    def read_tuple(i):
+        return (name_blob[10 * i:10 * i + 10].decode(), seq_blob[m * i:m * i + m].decode(), "I" * m)
 
     for _ in range(args.warmup):
         batch.run()
@@ -140,11 +198,13 @@ def main():
         sms += st.search_ms
     torch.cuda.synchronize()
     barrier()
-    dt = gdist.max_over_ranks(time.perf_counter() - t0)
+    mine = time.perf_counter() - t0
+    rank_times = gdist.all_gather_floats(mine)
+    dt = max(rank_times)
 
     # host pipeline (first bullet): the whole path for one batch outside the timed
     # region -- reads from host memory to HBM (batch create), kernels, records back to the host and SAM
-    # text formatted (16 host threads) -- reported beside `value`, never as it
+    # text -- reported beside `value`, never as it
     pipe = None
     if rank == 0 and not args.no_pipeline:
         t0 = time.perf_counter()
@@ -161,108 +221,128 @@ def main():
         log("host pipeline: %.0f reads/s (setup %.2fs, kernels %.2fs, SAM %.2fs, %.2f GB)"
             % (pipe["reads_per_s"], t1 - t0, t2 - t1, t3 - t2, nbytes / 1e9))
 
-    nres = min(args.check, reads_per_step)
-    sam, off = batch.results(0, nres)
+    counters = batch.read_counters()  # also fetches the records (stats below)
     st = batch.stats()
     total_reads = reads_per_step * args.steps * world
     value = total_reads / dt
+    deep = np.nonzero(counters[:, 12] >= 1)[0]
 
-    # parity spot check of this rank's first reads against the oracle (checker only)
+    # parity (checker only): a random sample of this rank's reads plus every read a search tier >= 1
+    # ran, GPU SAM against the oracle.  The oracle index takes the GPU suffix arrays only after an
+    # independent check of them (permutation + sampled adjacent-rotation order, oracle C++).
     parity = None
-    if args.check and rank == 0:
+    oi = None
+    if rank == 0 and (args.check or (not args.no_cpu and args.cpu_sample > 0)):
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle as O
         t0 = time.time()
-        oi = O.Index.from_arrays(codes, names, lengths, sa_f=gi.suffixArray(0), sa_r=gi.suffixArray(1))
-        t_oidx = time.time() - t0
-        nchk = nres
-        exp = oi.align(reads[:nchk], O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]))
-        got = sam
-        parity = {"reads": nchk, "identical": got == exp}
-        log("parity on %d reads: %s (oracle index %.1fs)" % (nchk, got == exp, t_oidx))
+        sa_f, sa_r = gi.suffixArray(0), gi.suffixArray(1)
+        O.check_cyclic_sa(codes, sa_f, samples=args.sa_check, seed=11, threads=host_cores()[0])
+        O.check_cyclic_sa(np.ascontiguousarray(codes[::-1]), sa_r, samples=args.sa_check, seed=12,
+                          threads=host_cores()[0])
+        t_sa = time.time() - t0
+        log("GPU suffix arrays pass the independent check (%d sampled pairs per strand): %.1fs" % (args.sa_check, t_sa))
+        oi = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
+        del sa_f, sa_r
+        t_oidx = time.time() - t0 - t_sa
+    if args.check and rank == 0:
+        rng = np.random.default_rng(7)
+        samp = np.unique(np.concatenate([rng.choice(reads_per_step, min(args.check, reads_per_step), replace=False),
+                                         deep])).astype(np.uint32)
+        got, _ = batch.results_select(samp)
+        sreads = [read_tuple(int(i)) for i in samp]
+        exp = oi.align(sreads, O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]),
+                       threads=host_cores()[0])
+        parity = {"reads": int(len(samp)), "random": int(min(args.check, reads_per_step)), "tier_ge1": int(len(deep)),
+                  "identical": got == exp, "sa_check_pairs": args.sa_check,
+                  "note": "random reads + every read of search tiers >= 1; oracle index from the GPU suffix arrays "
+                          "after an independent permutation + adjacent-order check"}
+        log("parity on %d reads (%d from tiers >= 1): %s (oracle index %.1fs)" % (len(samp), len(deep), got == exp, t_oidx))
 
-    # CPU baseline: the oracle (single-thread C++ restatement of the reference path) on this host.
-    # (i) 1 thread, as the reference runs (A/Align.java:174-196); (ii) T threads over contiguous read
-    # ranges.  cpu_baseline reports (ii); (i) is kept in detail.
+    # CPU baseline: the oracle (C++ restatement of the reference path) on this host.
+    # (i) 1 thread, as the reference runs (A/Align.java:174-196); (ii) every core this process may use,
+    # contiguous read ranges.  cpu_baseline reports (ii); (i) is kept in detail.
     cpu = cpu1 = None
     if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle as O
-        if parity is None:
-            oi = O.Index.from_arrays(codes, names, lengths, sa_f=gi.suffixArray(0), sa_r=gi.suffixArray(1))
-        ns = min(args.cpu_sample, len(reads))
+        T, tdesc = host_cores()
+        if args.cpu_threads:
+            T = args.cpu_threads
+        model = cpu_model()
+        ocfg = O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy])
+        ns = min(args.cpu_sample, reads_per_step)
+        r1 = [read_tuple(i) for i in range(ns)]
         t0 = time.perf_counter()
-        oi.align(reads[:ns], O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]))
+        oi.align(r1, ocfg)
         ct = time.perf_counter() - t0
-        model = "unknown CPU"
-        try:
-            with open("/proc/cpuinfo") as f:
-                model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), model)
-        except OSError:
-            pass
-        cpu1 = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port",
+        cpu1 = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port", "seconds": ct,
                 "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the reference "
                           "%s path (oracle/; CPU restatement, not the JVM), same index; %s"
                           % (ns, args.strategy.upper(), model)}
         log("cpu baseline (1 thread): %.0f reads/s (%d reads in %.1fs)" % (ns / ct, ns, ct))
         cpu = cpu1
-        T = max(1, args.cpu_threads)
-        nt = min(args.cpu_sample_mt, len(reads))
-        if T > 1 and nt > 0:
+        if T > 1:
+            nt = int(min(reads_per_step, max(ns, args.cpu_seconds * cpu1["value"] * T)))
+            rt = r1 + [read_tuple(i) for i in range(ns, nt)]
             t0 = time.perf_counter()
-            oi.align(reads[:nt], O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]), threads=T)
+            oi.align(rt, ocfg, threads=T)
             ct = time.perf_counter() - t0
-            cpu = {"value": nt / ct, "unit": "reads/s", "cores": T, "kind": "port",
-                   "sample": "first %d reads of rank 0's batch on %d host threads (contiguous ranges, one "
-                             "Aligner each), C++ restatement of the reference %s path (oracle/; CPU "
-                             "restatement, not the JVM), same index; %s" % (nt, T, args.strategy.upper(), model)}
+            cpu = {"value": nt / ct, "unit": "reads/s", "cores": T, "kind": "port", "seconds": ct,
+                   "sample": "first %d reads of rank 0's batch on %d host threads (%s; contiguous ranges, one "
+                             "Aligner each), C++ restatement of the reference %s path (oracle/; CPU restatement, "
+                             "not the JVM), same index; %s" % (nt, T, tdesc, args.strategy.upper(), model)}
             log("cpu baseline (%d threads): %.0f reads/s (%d reads in %.1fs)" % (T, nt / ct, nt, ct))
 
-    # roofline of the dominant kernel.  Algorithmic bytes = the bytes this path's algorithm must read
-    # (DESIGN.md §5): 64 B per Occ block of every FM step that reads one, 8 B per k-mer interval-table
-    # lookup, 3/8 B (2-bit base + N bit) per FM step answered from the text (single-row interval),
-    # 4 B per suffix-array gather.  `ref_equiv_bytes` prices every reference FM step at the SURVEY.md
-    # §8d lower bound of one 64-B block instead (what the reference's algorithm would read).
+    # Roofline of the dominant kernel.  `achieved` / `frac` follow SURVEY.md §8(d): 64 B per
+    # reference FM step (one Occ block, the lower bound of §8d's 1-2 blocks), 4 B per SA gather, and
+    # for each DP verification ceil(2n/8) + ceil(n/8) B of reference window + 32 B of Peq per 64-base
+    # block.  `kernel_bytes` re-prices what the kernels actually read: 64 B per Occ block read, 8 B per
+    # k-mer table lookup, 3/8 B per FM step answered from the 2-bit text (single-row interval).
     steps = args.steps
     q_ms, s_ms = qms / steps, sms / steps
     q_bytes = 64.0 * st.quick_blocks + 8.0 * st.kmer_lookups + 0.375 * st.quick_short_steps + 4.0 * st.quick_sa_reads
     q_ref = 64.0 * (st.quick_blocks + st.quick_short_steps) + 4.0 * st.quick_sa_reads
     s_bytes = (64.0 * (st.blocks - st.quick_blocks) + 0.375 * st.search_short_steps
-               + 4.0 * (st.sa_reads - st.quick_sa_reads))
-    s_ref = 64.0 * (st.blocks - st.quick_blocks + st.search_short_steps) + 4.0 * (st.sa_reads - st.quick_sa_reads)
+               + 4.0 * (st.sa_reads - st.quick_sa_reads) + st.verify_bytes)
+    s_ref = (64.0 * (st.blocks - st.quick_blocks + st.search_short_steps) + 4.0 * (st.sa_reads - st.quick_sa_reads)
+             + st.verify_bytes)
     if q_ms >= s_ms:
-        dom, ach_bytes, dom_ms, dom_ref = "fm_quickscan", q_bytes, q_ms, q_ref
+        dom, k_bytes, dom_ms, dom_ref = "fm_quickscan", q_bytes, q_ms, q_ref
     else:
-        dom, ach_bytes, dom_ms, dom_ref = args.strategy + "_search", s_bytes, s_ms, s_ref
-    achieved = ach_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        dom, k_bytes, dom_ms, dom_ref = args.strategy + "_search", s_bytes, s_ms, s_ref
+    gbs = (lambda b, ms: b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0)
     workload = ("%s; %d x %d bp reads per GPU per step, %s, -k %g, -m %s, besthit"
                 % (gname, reads_per_step, m, "0-5 edits (subs/1-bp indels)" if c4 else "0-2 substitutions", args.k,
                    args.strategy))
     traffic, traffic_src = _pmc_traffic(dom, workload)
     out = {
-        "metric": METRIC if not c4 else "reads/sec, 150 bp k<=5 with indels vs hg19 (config C4)", "value": value, "unit": "reads/s", "n_gpus": world, "steps": steps,
+        "metric": METRIC if not c4 else "reads/sec, 150 bp k<=5 with indels vs hg19 (config C4)", "value": value,
+        "unit": "reads/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "config": {"workload": workload,
                    "genome_bp": int(len(codes)), "reads_per_gpu_per_step": reads_per_step,
                    "parallelism": "reads sharded, index replicated (%d GPU)" % world},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": ach_bytes, "avg_launch_ms": dom_ms,
-                     "ref_equiv_bytes_per_launch": dom_ref},
+        "roofline": {"bound": "hbm", "kernel": dom, "definition": "SURVEY.md 8(d) algorithmic bytes",
+                     "achieved": gbs(dom_ref, dom_ms), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs(dom_ref, dom_ms) / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": dom_ref, "avg_launch_ms": dom_ms,
+                     "kernel_bytes_per_launch": k_bytes, "kernel_bytes_achieved": gbs(k_bytes, dom_ms),
+                     "kernel_bytes_frac": gbs(k_bytes, dom_ms) / HBM_PEAK_GBS},
         "cpu_baseline": cpu,
-        "detail": {"quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
+        "detail": {"rank_seconds": rank_times, "devices": "rank r on GPU r mod %d" % torch.cuda.device_count(),
+                   "quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
                    "fm_searches_per_read": st.fm_searches / reads_per_step,
                    "quick_steps_per_read": st.quick_steps / reads_per_step,
                    "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
-                   "tier_ms": [round(x, 3) for x in st.tier_ms],
+                   "tier_ms": [round(x, 3) for x in st.tier_ms], "dp_verifications_per_read": st.num_sw / reads_per_step,
                    "quick_short_steps_per_read": st.quick_short_steps / reads_per_step,
                    "cpu_baseline_1thread": cpu1, "host_pipeline": pipe,
                    "search_short_steps_per_read": st.search_short_steps / reads_per_step,
-                   "rank_kernel": {"kernel": "fm_quickscan", "algorithmic_bytes_per_launch": q_bytes,
-                                   "ref_equiv_bytes_per_launch": q_ref, "avg_launch_ms": q_ms,
-                                   "achieved_GBs": q_bytes / (q_ms * 1e-3) / 1e9 if q_ms > 0 else 0.0,
-                                   "frac": (q_bytes / (q_ms * 1e-3) / 1e9 if q_ms > 0 else 0.0) / HBM_PEAK_GBS,
+                   "rank_kernel": {"kernel": "fm_quickscan", "definition": "SURVEY.md 8(d) algorithmic bytes",
+                                   "algorithmic_bytes_per_launch": q_ref, "avg_launch_ms": q_ms,
+                                   "achieved_GBs": gbs(q_ref, q_ms), "frac": gbs(q_ref, q_ms) / HBM_PEAK_GBS,
+                                   "kernel_bytes_per_launch": q_bytes, "kernel_bytes_GBs": gbs(q_bytes, q_ms),
+                                   "kernel_bytes_frac": gbs(q_bytes, q_ms) / HBM_PEAK_GBS,
                                    "traffic": _pmc_traffic("fm_quickscan", workload)[0]},
                    "mapped": st.n_mapped, "unmapped": st.n_unmapped, "index_build_s": t_index,
                    "index_gb": gi.deviceBytes() / 1e9, "parity": parity},

@@ -313,6 +313,7 @@ struct BsfLane {
   int status;  // ST_*
   // instrumentation
   int quickSteps, blocks, saReads, maxHeap, kmerLookups, shortSteps, textSteps;
+  int numSW, verifyBytes;  // DP verifications and their §8d bytes (instrumentation)
   // debug trace (nullptr in production launches): 4 words per event
   uint32_t *trace = nullptr;
   int traceCap = 0, traceN = 0;
@@ -1170,6 +1171,8 @@ struct BsfLane {
     const int kb = cfg.bandWidth;
     const int bMax = mq + w - 1 >= w ? (mq + w - 1) / w : 1;
     const int N = (int)(refEnd - refStart);
+    ++numSW;
+    verifyBytes += (2 * N + 7) / 8 + (N + 7) / 8 + 32 * bMax;
     if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || 4 * ((N >> 2) + 1) > caps.wr) { status = ST_OVERFLOW; return -1; }
     uint64_t pA[DB], pC[DB], pG[DB], pT[DB];
 #pragma unroll
@@ -1667,12 +1670,14 @@ struct BsfLane {
   // ---- AlignmentProcess.align_internal (:278-477), split at the quick scan ----
   // Phase 1 (fm_quickscan kernel): N check, FMQuickScan on both strands, exact hits.
   // Returns 1 when the read needs the best-first search; otherwise the result is final.
-  GWA_HD int quickPhase(ScanRes *sr, OutHeader *oh, OutHit *oHits, uint16_t *oCig) {
+  GWA_HD int quickPhase(ScanRes *sr, OutHeader *oh, const OutSlots &os, uint32_t rd_) {
     oh->fmSearches = 0;
     oh->states = 0;
     oh->searchBlocks = 0;
     oh->saReads = 0;
     oh->searchShort = 0;
+    oh->numSW = oh->verifyBytes = 0;
+    oh->poolFail = 0;
     oh->nChains = oh->nHits = oh->nCigar = 0;
     oh->status = ST_UNMAPPED;
     {
@@ -1680,9 +1685,9 @@ struct BsfLane {
       if (countN > k) { finishQuick(oh); return 0; }
     }
     Scan sF = quickScan(0);
-    if (sF.numMismatches == 0) { reportExact(sF, 0, oh, oHits, oCig); return 0; }
+    if (sF.numMismatches == 0) { reportExact(sF, 0, oh, os, rd_); return 0; }
     Scan sR = quickScan(1);
-    if (sR.numMismatches == 0) { reportExact(sR, 1, oh, oHits, oCig); return 0; }
+    if (sR.numMismatches == 0) { reportExact(sR, 1, oh, os, rd_); return 0; }
     if (k == 0) { finishQuick(oh); return 0; }
     sr->nmF = sF.numMismatches; sr->lmF = sF.lmStart;
     sr->nmR = sR.numMismatches; sr->lmR = sR.lmStart;
@@ -1698,7 +1703,7 @@ struct BsfLane {
   }
   // reportExactMatchAlignment (:490-494) + FMIndexOnGenome.toGenomeCoordinate (:258-269):
   // the single exact ReadHit is the reported BESTHIT/ALLHITS/TOPL result.
-  GWA_HD void reportExact(const Scan &s, int strand, OutHeader *oh, OutHit *oHits, uint16_t *oCig) {
+  GWA_HD void reportExact(const Scan &s, int strand, OutHeader *oh, const OutSlots &os, uint32_t rd_) {
     int64_t sav = s.uniq ? (int64_t)s.tp : (int64_t)ix.sa[strand == 0 ? 1 : 0][s.lb];
     if (!s.uniq) ++saReads;
     finishQuick(oh);
@@ -1707,11 +1712,12 @@ struct BsfLane {
     pos += 1;
     int32_t chr, p;
     if (pos < 0 || translate(pos, &chr, &p) != 0) { oh->status = ST_ERROR; return; }
-    OutHit &o = oHits[0];
+    oh->hitOff = rd_ * os.hitCap;
+    oh->cigOff = rd_ * os.cigCap;
+    OutHit &o = os.hits[oh->hitOff];
     o.chr = chr; o.pos = p; o.matchLength = m; o.qStart = 0; o.qEnd = m; o.diff = 0; o.strand = strand;
     o.numHits = (int32_t)(s.ub - s.lb); o.next = -1; o.cigarOff = 0; o.cigarLen = 1;
-    oCig[0] = (uint16_t)((m << 3) | 0);
-    oh->chainHead[0] = 0;
+    os.cig[oh->cigOff] = (uint16_t)((m << 3) | 0);
     oh->nChains = 1; oh->nHits = 1; oh->nCigar = 1;
     oh->status = ST_MAPPED;
   }
@@ -2054,44 +2060,67 @@ struct BsfLane {
       stairTab = st.tab + (stairBad ? 0 : b);
     }
     quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = textSteps = 0;
+    numSW = verifyBytes = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains
-  GWA_HD void writeSearchOutput(OutHeader *oh, OutHit *oHits, uint16_t *oCig, int outHitCap, int outCigCap) {
+  GWA_HD void writeSearchOutput(OutHeader *oh, const OutSlots &os, uint32_t rd_) {
     oh->fmSearches = numFMIndexSearches;
     oh->searchBlocks = blocks;
     oh->saReads = saReads;
     oh->searchShort = textSteps;
     oh->states = nStates;
     oh->maxHeap = maxHeap;
+    oh->numSW = numSW;
+    oh->verifyBytes = verifyBytes;
     oh->nChains = 0;
     oh->nHits = 0;
     oh->nCigar = 0;
+    oh->poolFail = 0;
     if (status == ST_OVERFLOW || status == ST_ERROR) { oh->status = status; return; }
     bool hasHitF = minMismatches <= k && listSize > 0;
     if (!hasHitF) { oh->status = ST_UNMAPPED; return; }
     int nRep = cfg.reportType == 0 ? 1 : cfg.reportType == 1 ? listSize : (cfg.topL < listSize ? cfg.topL : listSize);
-    if (nRep > 4) { oh->status = ST_OVERFLOW; return; }
-    int nh = 0, ncg = 0;
+    // room: the read's fixed slot, or a reservation in the shared pool (OutSlots)
+    uint32_t needH = 0, needC = 0;
+    for (int r = 0; r < nRep; ++r)
+      for (int t = L.list()[r]; t >= 0; t = L.hits()[t].next) {
+        ++needH;
+        needC += (uint32_t)L.hits()[t].cigarLen;
+      }
+    uint64_t hb = (uint64_t)rd_ * os.hitCap, cb = (uint64_t)rd_ * os.cigCap;
+    if (needH > os.hitCap || needC > os.cigCap) {
+      hb = os.poolHit0 + outReserve(os.poolUsed, needH);
+      cb = os.poolCig0 + outReserve(os.poolUsed + 1, needC);
+      if (hb + needH > os.poolHitEnd || cb + needC > os.poolCigEnd) {
+        outReserve(os.poolUsed + 2, 1);
+        oh->status = ST_OVERFLOW;
+        oh->poolFail = 1;
+        return;
+      }
+    }
+    OutHit *oHits = os.hits + hb;
+    uint16_t *oCig = os.cig + cb;
+    uint32_t nh = 0, ncg = 0;
     for (int r = 0; r < nRep; ++r) {
-      oh->chainHead[r] = nh;
       int prevOut = -1;
       for (int t = L.list()[r]; t >= 0; t = L.hits()[t].next) {
         const DHit &h = L.hits()[t];
-        if (nh >= outHitCap || ncg + h.cigarLen > outCigCap) { oh->status = ST_OVERFLOW; return; }
         OutHit &o = oHits[nh];
         o.chr = h.chr; o.pos = h.pos; o.matchLength = h.matchLength; o.qStart = h.qStart; o.qEnd = h.qEnd;
         o.diff = h.diff; o.strand = h.strand; o.numHits = h.numHits; o.next = -1;
-        o.cigarOff = (uint16_t)ncg;
-        o.cigarLen = (uint16_t)h.cigarLen;
+        o.cigarOff = ncg;
+        o.cigarLen = (uint32_t)h.cigarLen;
         for (int i = 0; i < h.cigarLen; ++i) oCig[ncg++] = L.cigar()[h.cigarOff + i];
-        if (prevOut >= 0) oHits[prevOut].next = nh;
-        prevOut = nh;
+        if (prevOut >= 0) oHits[prevOut].next = (int32_t)nh;
+        prevOut = (int)nh;
         ++nh;
       }
     }
+    oh->hitOff = (uint32_t)hb;
+    oh->cigOff = (uint32_t)cb;
     oh->nChains = nRep;
-    oh->nHits = nh;
-    oh->nCigar = ncg;
+    oh->nHits = (int32_t)nh;
+    oh->nCigar = (int32_t)ncg;
     oh->status = ST_MAPPED;
   }
 

@@ -10,7 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
-#include <sstream>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -73,13 +73,17 @@ struct gwa_index {
   int32_t *d_chrRank = nullptr;
   size_t bytes = 0;
   IndexView view{};
-  // reusable search scratch
+  // reusable search scratch: one batch at a time runs its kernels on the index (runMu); batch set-up
+  // (H2D) and results (D2H, SAM) run outside the lock on each batch's own stream, so several host
+  // threads can keep one device busy (gwa_pipeline)
   uint8_t *scratch = nullptr;
   size_t scratchBytes = 0;
+  std::mutex runMu;
 };
 
 struct gwa_batch {
   gwa_index *ix = nullptr;
+  hipStream_t stream = nullptr;
   gwa_config_t cfg{};
   SearchConfig scfg{};
   // host copy of the reads (SAM needs names, sequences, qualities)
@@ -102,14 +106,18 @@ struct gwa_batch {
   uint32_t *d_count = nullptr;  // [0] search list, [1 + t] overflow list of tier t, [8 + t] tier t work counter
   uint64_t *d_stair = nullptr;
   uint32_t *d_stairBase = nullptr;
-  int hitCap = 4, cigCap = 64;
+  uint32_t hitCap = 4, cigCap = 64;
+  uint64_t poolHits = 0, poolCig = 0;  // OutSlots pool behind the fixed slots (grown on demand)
+  uint64_t poolUsedH = 0, poolUsedC = 0;
   StairTables st{};
   // results
   std::vector<OutHeader> oh;
   std::vector<OutHit> hits;
   std::vector<uint16_t> cig;
   gwa_batch_stats_t stats{};
-  bool ran = false;
+  bool ran = false, fetched = false;
+  bool headerOnly = false;  // -m bd / -m bwa: the reference emits no SAM records (see gwa_batch_create)
+  std::vector<std::pair<uint32_t, int>> deep;  // (read, tier) of every read rerun on a tier >= 1
 };
 
 static void freeIndexDev(gwa_index *ix) {
@@ -132,48 +140,54 @@ bool cyclicSAGpu(const uint8_t *d_T, uint64_t N, uint32_t *d_sa, int alphabetBit
 void reverseTextGpu(const uint8_t *d_T, uint64_t N, uint8_t *d_R, hipStream_t s);
 void buildOccGpu(const uint8_t *d_T, const uint32_t *d_sa, uint64_t N, OccBlock *d_occ, hipStream_t s);
 void packTextGpu(const uint8_t *d_T, uint64_t N, uint64_t *d_text2, uint64_t *d_textN, hipStream_t s);
+void unpackTextGpu(const uint64_t *d_text2, const uint64_t *d_textN, uint64_t N, uint8_t *d_T, hipStream_t s);
+void countCodesGpu(const uint8_t *d_T, uint64_t N, unsigned long long *d_cnt5, hipStream_t s);
 }  // namespace gwa
 
-// Index construction in HBM (the `bwt` command's work, A/BWTransform.java:72-179): upload the
-// packed text once, build the reversed text, both cyclic SAs, both Occ-block arrays and the
-// 2-bit text on the GPU.
-static void finishAndUpload(gwa_index *ix) {
+// Index construction in HBM (the `bwt` command's work, A/BWTransform.java:72-179) from the text
+// codes already on the device (dT, N bytes; freed here): the reversed text, both cyclic SAs, both
+// Occ-block arrays, the 2-bit text (unless a saved index supplied it), the symbol counts, the contig
+// table and the k-mer tables.
+static void buildFromDeviceText(gwa_index *ix, uint8_t *dT) {
   HostIndex &h = ix->host;
-  if (h.N == 0) throw std::runtime_error("empty reference");
-  if (h.N >= 0xFFFFFFFFull) throw std::runtime_error("reference longer than 2^32-2 bases is not supported");
-  HIPCHK(hipSetDevice(ix->device));
-  HIPCHK(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
   hipStream_t s = ix->stream;
   const uint64_t N = h.N;
-  uint8_t *dT = devAlloc<uint8_t>(N);
-  uint8_t *dR = devAlloc<uint8_t>(N);
-  HIPCHK(hipMemcpyAsync(dT, h.T.data(), N, hipMemcpyHostToDevice, s));
-  reverseTextGpu(dT, N, dR, s);
-  ix->d_sa[0] = devAlloc<uint32_t>(N, &ix->bytes);
-  ix->d_sa[1] = devAlloc<uint32_t>(N, &ix->bytes);
-  // cyclic suffix arrays (A/sais/CyclicSAIS.java:223-431 computes the same unique order)
-  if (!cyclicSAGpu(dT, N, ix->d_sa[0], 3, s) || !cyclicSAGpu(dR, N, ix->d_sa[1], 3, s)) {
+  uint8_t *dR = nullptr;
+  try {
+    dR = devAlloc<uint8_t>(N);
+    reverseTextGpu(dT, N, dR, s);
+    ix->d_sa[0] = devAlloc<uint32_t>(N, &ix->bytes);
+    ix->d_sa[1] = devAlloc<uint32_t>(N, &ix->bytes);
+    // cyclic suffix arrays (A/sais/CyclicSAIS.java:223-431 computes the same unique order)
+    if (!cyclicSAGpu(dT, N, ix->d_sa[0], 3, s) || !cyclicSAGpu(dR, N, ix->d_sa[1], 3, s))
+      throw std::runtime_error("reference text is periodic (cyclic rotations tie): unsupported");
+    const uint64_t nb = N / 128 + 1;
+    ix->d_occ[0] = devAlloc<OccBlock>(nb, &ix->bytes);
+    ix->d_occ[1] = devAlloc<OccBlock>(nb, &ix->bytes);
+    buildOccGpu(dT, ix->d_sa[0], N, ix->d_occ[0], s);
+    buildOccGpu(dR, ix->d_sa[1], N, ix->d_occ[1], s);
+    if (!ix->d_text2) {
+      const uint64_t nw = N / 64 + 1;
+      ix->d_text2 = devAlloc<uint64_t>(2 * nw, &ix->bytes);
+      ix->d_textN = devAlloc<uint64_t>(nw, &ix->bytes);
+      packTextGpu(dT, N, ix->d_text2, ix->d_textN, s);
+    }
+    // CharacterCount.C (A/CharacterCount.java:41-50)
+    unsigned long long *dCnt = devAlloc<unsigned long long>(5);
+    countCodesGpu(dT, N, dCnt, s);
+    unsigned long long count[5];
+    HIPCHK(hipMemcpyAsync(count, dCnt, sizeof(count), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    (void)hipFree(dCnt);
+    uint64_t sum = 0;
+    for (int c = 0; c < 5; ++c) { h.C[c] = sum; sum += count[c]; }
+  } catch (...) {
     (void)hipFree(dT);
-    (void)hipFree(dR);
-    throw std::runtime_error("reference text is periodic (cyclic rotations tie): unsupported");
+    if (dR) (void)hipFree(dR);
+    throw;
   }
-  const uint64_t nb = N / 128 + 1;
-  ix->d_occ[0] = devAlloc<OccBlock>(nb, &ix->bytes);
-  ix->d_occ[1] = devAlloc<OccBlock>(nb, &ix->bytes);
-  buildOccGpu(dT, ix->d_sa[0], N, ix->d_occ[0], s);
-  buildOccGpu(dR, ix->d_sa[1], N, ix->d_occ[1], s);
-  const uint64_t nw = N / 64 + 1;
-  ix->d_text2 = devAlloc<uint64_t>(2 * nw, &ix->bytes);
-  ix->d_textN = devAlloc<uint64_t>(nw, &ix->bytes);
-  packTextGpu(dT, N, ix->d_text2, ix->d_textN, s);
-  HIPCHK(hipStreamSynchronize(s));
   (void)hipFree(dT);
   (void)hipFree(dR);
-  // CharacterCount.C (A/CharacterCount.java:41-50)
-  uint64_t count[5] = {0, 0, 0, 0, 0};
-  for (uint64_t i = 0; i < N; ++i) count[h.T[i] > 4 ? 4 : h.T[i]]++;
-  uint64_t sum = 0;
-  for (int c = 0; c < 5; ++c) { h.C[c] = sum; sum += count[c]; }
   rankNames(h);
   ix->d_contig = devUpload(h.offsets, s, &ix->bytes);
   ix->d_chrRank = devUpload(h.chrRank, s, &ix->bytes);
@@ -198,7 +212,36 @@ static void finishAndUpload(gwa_index *ix) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
   }
-  std::vector<uint8_t>().swap(h.T);  // the text lives in HBM from here on
+}
+
+static void checkSize(const HostIndex &h) {
+  if (h.N == 0) throw std::runtime_error("empty reference");
+  if (h.N >= 0xFFFFFFFFull) throw std::runtime_error("reference longer than 2^32-2 bases is not supported");
+}
+
+// from the host text codes (h.T, released afterwards: the text lives in HBM from here on)
+static void finishAndUpload(gwa_index *ix) {
+  HostIndex &h = ix->host;
+  checkSize(h);
+  HIPCHK(hipSetDevice(ix->device));
+  HIPCHK(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
+  uint8_t *dT = devAlloc<uint8_t>(h.N);
+  HIPCHK(hipMemcpyAsync(dT, h.T.data(), h.N, hipMemcpyHostToDevice, ix->stream));
+  buildFromDeviceText(ix, dT);
+  std::vector<uint8_t>().swap(h.T);
+}
+
+// from a saved index's 2-bit text + N bitmap (gwa_index_save)
+static void loadPacked(gwa_index *ix, const std::vector<uint64_t> &text2, const std::vector<uint64_t> &textN) {
+  HostIndex &h = ix->host;
+  checkSize(h);
+  HIPCHK(hipSetDevice(ix->device));
+  HIPCHK(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
+  ix->d_text2 = devUpload(text2, ix->stream, &ix->bytes);
+  ix->d_textN = devUpload(textN, ix->stream, &ix->bytes);
+  uint8_t *dT = devAlloc<uint8_t>(h.N);
+  unpackTextGpu(ix->d_text2, ix->d_textN, h.N, dT, ix->stream);
+  buildFromDeviceText(ix, dT);
 }
 
 extern "C" {
@@ -240,13 +283,121 @@ int gwa_index_build_fasta(const char *text, uint64_t len, int device, gwa_index_
   return buildCommon(ix, device, out);
 }
 
+// Saved index (gwa_index_save): the text as 2-bit words + N bitmap and the contig table; loading
+// rebuilds the suffix arrays, Occ blocks and k-mer tables on the GPU (seconds at hg19 size), which is
+// faster than reading their 30 GB from storage.  Layout (little endian):
+//   "GWAIDX1\n"  u64 N  u32 nContigs  u32 0  { u32 nameLen, name, i64 length } x nContigs
+//   u64 nw  u64 text2[2 * nw]  u64 textN[nw]          (nw = N / 64 + 1)
+static const char kIdxMagic[8] = {'G', 'W', 'A', 'I', 'D', 'X', '1', '\n'};
+
+static std::string readWholeFile(const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) throw std::runtime_error(std::string("cannot open ") + path);
+  std::string t;
+  if (fseek(f, 0, SEEK_END) == 0) {
+    const long sz = ftell(f);
+    if (sz > 0) t.resize((size_t)sz);
+    fseek(f, 0, SEEK_SET);
+  }
+  size_t got = t.empty() ? 0 : fread(&t[0], 1, t.size(), f);
+  t.resize(got);
+  char buf[1 << 16];
+  size_t r;
+  while ((r = fread(buf, 1, sizeof buf, f)) > 0) t.append(buf, r);  // (non-seekable input)
+  fclose(f);
+  return t;
+}
+
 int gwa_index_open(const char *path, int device, gwa_index_t **out) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) return fail(std::string("cannot open ") + path);
-  std::stringstream ss;
-  ss << f.rdbuf();
-  std::string t = ss.str();
-  return gwa_index_build_fasta(t.data(), t.size(), device, out);
+  gwa_index *ix = nullptr;
+  try {
+    const std::string t = readWholeFile(path);
+    if (t.size() < 8 || memcmp(t.data(), kIdxMagic, 8) != 0)
+      return gwa_index_build_fasta(t.data(), t.size(), device, out);
+    ix = new gwa_index();
+    HostIndex &h = ix->host;
+    size_t pos = 8;
+    auto get = [&](void *dst, size_t n) {
+      if (pos + n > t.size()) throw std::runtime_error(std::string("truncated index file ") + path);
+      memcpy(dst, t.data() + pos, n);
+      pos += n;
+    };
+    uint64_t N = 0;
+    uint32_t nc = 0, zero = 0;
+    get(&N, 8);
+    get(&nc, 4);
+    get(&zero, 4);
+    int64_t off = 0;
+    for (uint32_t i = 0; i < nc; ++i) {
+      uint32_t ln = 0;
+      get(&ln, 4);
+      std::string nm(ln, '\0');
+      if (ln) get(&nm[0], ln);
+      int64_t L = 0;
+      get(&L, 8);
+      h.names.push_back(nm);
+      h.offsets.push_back(off);
+      h.lengths.push_back(L);
+      off += L;
+    }
+    if ((uint64_t)off != N) throw std::runtime_error(std::string("corrupt index file (contig lengths) ") + path);
+    uint64_t nw = 0;
+    get(&nw, 8);
+    if (nw != N / 64 + 1) throw std::runtime_error(std::string("corrupt index file (text size) ") + path);
+    std::vector<uint64_t> text2(2 * nw), textN(nw);
+    get(text2.data(), text2.size() * 8);
+    get(textN.data(), textN.size() * 8);
+    h.N = N;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) throw std::runtime_error("no HIP device: the gwa align path requires an MI355X GPU");
+    if (device < 0 || device >= nd) throw std::runtime_error("invalid device " + std::to_string(device));
+    ix->device = device;
+    loadPacked(ix, text2, textN);
+    *out = ix;
+    return 0;
+  } catch (std::exception &e) {
+    if (ix) {
+      freeIndexDev(ix);
+      delete ix;
+    }
+    return fail(e.what());
+  }
+}
+
+int gwa_index_save(const gwa_index_t *ix, const char *path) {
+  FILE *f = nullptr;
+  try {
+    const HostIndex &h = ix->host;
+    const uint64_t N = h.N, nw = N / 64 + 1;
+    std::vector<uint64_t> text2(2 * nw), textN(nw);
+    HIPCHK(hipSetDevice(ix->device));
+    HIPCHK(hipMemcpy(text2.data(), ix->d_text2, text2.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(textN.data(), ix->d_textN, textN.size() * 8, hipMemcpyDeviceToHost));
+    f = fopen(path, "wb");
+    if (!f) throw std::runtime_error(std::string("cannot create ") + path);
+    auto put = [&](const void *p, size_t n) {
+      if (n && fwrite(p, 1, n, f) != n) throw std::runtime_error(std::string("write failed: ") + path);
+    };
+    const uint32_t nc = (uint32_t)h.names.size(), zero = 0;
+    put(kIdxMagic, 8);
+    put(&N, 8);
+    put(&nc, 4);
+    put(&zero, 4);
+    for (uint32_t i = 0; i < nc; ++i) {
+      const uint32_t ln = (uint32_t)h.names[i].size();
+      put(&ln, 4);
+      put(h.names[i].data(), ln);
+      put(&h.lengths[i], 8);
+    }
+    put(&nw, 8);
+    put(text2.data(), text2.size() * 8);
+    put(textN.data(), textN.size() * 8);
+    if (fclose(f) != 0) { f = nullptr; throw std::runtime_error(std::string("write failed: ") + path); }
+    return 0;
+  } catch (std::exception &e) {
+    if (f) fclose(f);
+    return fail(e.what());
+  }
 }
 
 int gwa_index_build_codes(const uint8_t *codes, uint64_t n, int32_t n_contigs, const char *const *names,
@@ -275,6 +426,7 @@ uint64_t gwa_index_device_bytes(const gwa_index_t *ix) { return ix->bytes; }
 int gwa_index_export_sa(const gwa_index_t *ix, int strand, uint32_t *out) {
   if (strand < 0 || strand > 1) return fail("strand must be 0 or 1");
   try {
+    HIPCHK(hipSetDevice(ix->device));
     HIPCHK(hipMemcpy(out, ix->d_sa[strand], ix->host.N * sizeof(uint32_t), hipMemcpyDeviceToHost));
   } catch (std::exception &e) {
     return fail(e.what());
@@ -304,16 +456,27 @@ static void freeBatchDev(gwa_batch *b) {
                 b->d_stair, b->d_stairBase};
   for (void *p : ps)
     if (p) (void)hipFree(p);
+  if (b->stream) (void)hipStreamDestroy(b->stream);
+  b->stream = nullptr;
 }
 
 int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_batch_t **out) {
   auto *b = new gwa_batch();
   try {
-    if (cfg->strategy != 0 && cfg->strategy != 1)
-      throw std::runtime_error("only -m bsf and -m sf are implemented on the device path");
+    if (cfg->strategy < 0 || cfg->strategy > 3) throw std::runtime_error("unknown strategy (-m bsf, sf, bd, bwa)");
     HIPCHK(hipSetDevice(ix->device));
     b->ix = ix;
     b->cfg = *cfg;
+    if (cfg->strategy >= 2) {
+      // -m bd / -m bwa (A/Align.java:124-132): BidirectionalBWT reports BWAState / AlignmentSA objects,
+      // which SAMOutput.emit drops (it prints AlignmentRecord only, A/SAMOutput.java:73-82), so the
+      // reference's SAM is the header alone.  Same output here, without a search whose results no one
+      // reads.
+      b->headerOnly = true;
+      b->n = reads->n;
+      *out = b;
+      return 0;
+    }
     SearchConfig &sc = b->scfg;
     sc.k = cfg->k; sc.reportType = cfg->report_type; sc.topL = cfg->top_l; sc.numSplit = cfg->num_split;
     sc.matchScore = cfg->match; sc.mismatchPenalty = cfg->mismatch; sc.splitOpenPenalty = cfg->split_open;
@@ -389,7 +552,8 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     std::vector<uint64_t> tab;
     std::vector<uint32_t> base;
     buildStairTables(lens, std::max(b->kmax, 0), tab, base);
-    hipStream_t s = ix->stream;
+    HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    hipStream_t s = b->stream;
     b->d_codes = devUpload(b->codes, s, nullptr);
     b->d_off = devUpload(b->codeOff, s, nullptr);
     b->d_len = devUpload(b->codeLen, s, nullptr);
@@ -408,13 +572,22 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
         b->st.ldsCount = (uint32_t)cnt;
       }
     }
-    const int chains = cfg->report_type == 0 ? 1 : 4;
-    b->hitCap = chains * std::max(1, cfg->num_split + 1);
-    b->cigCap = 64 * chains;
+    // fixed output slot per read: the chains besthit / a small -L report; more go to the pool
+    const int chains = cfg->report_type == 0 ? 1 : cfg->report_type == 2 ? std::max(1, std::min(cfg->top_l, 4)) : 2;
+    b->hitCap = (uint32_t)(chains * std::max(1, cfg->num_split + 1));
+    b->cigCap = (uint32_t)(64 * chains);
+    b->poolHits = std::max<uint64_t>(1 << 16, (uint64_t)n * b->hitCap / 16);
+    b->poolCig = std::max<uint64_t>(1 << 20, (uint64_t)n * b->cigCap / 16);
+    if (const char *e = getenv("GWA_OUT_POOL")) {  // initial pool size in hits (tests: force growth)
+      b->poolHits = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+      b->poolCig = 64 * b->poolHits;
+    }
+    if ((uint64_t)n * b->cigCap + b->poolCig >= 0xFFFFFFFFull)
+      throw std::runtime_error("read batch too large for 32-bit output offsets: use fewer reads per batch");
     b->d_sres = devAlloc<ScanRes>(n);
     b->d_oh = devAlloc<OutHeader>(n);
-    b->d_hits = devAlloc<OutHit>((size_t)n * b->hitCap);
-    b->d_cig = devAlloc<uint16_t>((size_t)n * b->cigCap);
+    b->d_hits = devAlloc<OutHit>((size_t)n * b->hitCap + b->poolHits);
+    b->d_cig = devAlloc<uint16_t>((size_t)n * b->cigCap + b->poolCig);
     b->d_list[0] = devAlloc<uint32_t>(n);
     b->d_list[1] = devAlloc<uint32_t>(n);
     b->d_count = devAlloc<uint32_t>(16);
@@ -455,33 +628,77 @@ static const Tier kSfTiers[kNumTiers] = {
     {65536, 65536, 4096, 4096, 65536, 16384, 1024u},
 };
 
+// the batch's output slots + pool (gwa_layout.h OutSlots); pool counters at d_count[12..14]
+static OutSlots outSlots(const gwa_batch *b) {
+  OutSlots o;
+  o.hits = b->d_hits;
+  o.cig = b->d_cig;
+  o.hitCap = b->hitCap;
+  o.cigCap = b->cigCap;
+  o.poolUsed = b->d_count + 12;
+  o.poolHit0 = (uint64_t)b->n * b->hitCap;
+  o.poolHitEnd = o.poolHit0 + b->poolHits;
+  o.poolCig0 = (uint64_t)b->n * b->cigCap;
+  o.poolCigEnd = o.poolCig0 + b->poolCig;
+  return o;
+}
+
+// Grow the output pool to hold at least twice what has been reserved so far.  Offsets are absolute
+// indices into the hit / CIGAR arrays, so what the kernels already wrote is copied as it lies.
+static void growPool(gwa_batch *b, uint64_t usedH, uint64_t usedC, hipStream_t s) {
+  const uint64_t nh = std::max<uint64_t>(2 * b->poolHits, 2 * usedH), nc = std::max<uint64_t>(2 * b->poolCig, 2 * usedC);
+  const uint64_t fh = (uint64_t)b->n * b->hitCap, fc = (uint64_t)b->n * b->cigCap;
+  if (fc + nc >= 0xFFFFFFFFull || fh + nh >= 0xFFFFFFFFull)
+    throw std::runtime_error("reported hits exceed the 32-bit output offsets: use fewer reads per batch");
+  OutHit *h = devAlloc<OutHit>(fh + nh);
+  uint16_t *c = devAlloc<uint16_t>(fc + nc);
+  HIPCHK(hipMemcpyAsync(h, b->d_hits, (fh + b->poolHits) * sizeof(OutHit), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(c, b->d_cig, (fc + b->poolCig) * sizeof(uint16_t), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  (void)hipFree(b->d_hits);
+  (void)hipFree(b->d_cig);
+  b->d_hits = h;
+  b->d_cig = c;
+  b->poolHits = nh;
+  b->poolCig = nc;
+}
+
+namespace {
+struct Events {  // destroyed on every path out of gwa_batch_run
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  Events() {
+    for (auto &x : e) HIPCHK(hipEventCreate(&x));
+  }
+  ~Events() {
+    for (auto &x : e)
+      if (x) (void)hipEventDestroy(x);
+  }
+};
+}  // namespace
+
 int gwa_batch_run(gwa_batch_t *b) {
   try {
     gwa_index *ix = b->ix;
     HIPCHK(hipSetDevice(ix->device));
-    hipStream_t s = ix->stream;
+    hipStream_t s = b->stream;
+    std::lock_guard<std::mutex> runLock(ix->runMu);
     memset(&b->stats, 0, sizeof(b->stats));
+    if (b->headerOnly) {
+      b->ran = true;
+      return 0;
+    }
+    b->ran = b->fetched = false;
+    b->poolUsedH = b->poolUsedC = 0;
+    b->deep.clear();
     ReadsView rv{b->d_codes, b->d_off, b->d_len, b->n};
-    hipEvent_t e0, e1, e2;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventCreate(&e2));
+    Events ev;
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1], e2 = ev.e[2];
     HIPCHK(hipMemsetAsync(b->d_count, 0, 16 * sizeof(uint32_t), s));
     HIPCHK(hipEventRecord(e0, s));
     const bool sf = b->cfg.strategy == 1;
-    const char *qtre = sf ? nullptr : getenv("GWA_QTRACE_READ");
-    static uint32_t *d_qtrace = nullptr;
-    if (qtre && !d_qtrace) { HIPCHK(hipMalloc(&d_qtrace, 4 * 65540)); HIPCHK(hipMemset(d_qtrace, 0, 4 * 65540)); }
     if (!sf)
-      launchQuickscan(b->maxM <= 128 ? 4 : 8, ix->view, b->scfg, rv, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->hitCap,
-                      b->cigCap, b->d_list[0], b->d_count, s, qtre ? d_qtrace : nullptr, qtre ? atoi(qtre) : -1);
-    if (qtre) {
-      std::vector<uint32_t> tv(65537);
-      HIPCHK(hipMemcpyAsync(tv.data(), d_qtrace, 4 * 65537, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      FILE *tf = fopen("gpurun_out/gpu_qtrace.bin", "wb");
-      if (tf) { fwrite(tv.data(), 4, 1 + tv[0], tf); fclose(tf); }
-    }
+      launchQuickscan(b->maxM <= 128 ? 4 : 8, ix->view, b->scfg, rv, b->d_sres, b->d_oh, outSlots(b), b->d_list[0],
+                      b->d_count, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
     uint32_t nSearch = b->n;
@@ -494,7 +711,8 @@ int gwa_batch_run(gwa_batch_t *b) {
     int cur = 0;
     uint32_t n = nSearch;
     const int m = std::max(b->maxM, 1);
-    for (int t = 0; t < kNumTiers && n > 0; ++t) {
+    int t = 0, regrow = 0;
+    while (n > 0) {
       const Tier &T = sf ? kSfTiers[t] : kTiers[t];
       Caps caps;
       caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
@@ -516,18 +734,17 @@ int gwa_batch_run(gwa_batch_t *b) {
         ix->scratchBytes = need;
       }
       uint32_t *ovfCount = b->d_count + 1 + t;
+      HIPCHK(hipMemsetAsync(ovfCount, 0, 4, s));
+      HIPCHK(hipMemsetAsync(b->d_count + 8 + t, 0, 4, s));
       HIPCHK(hipEventRecord(e1, s));
-      static uint32_t *d_trace = nullptr;
-      const char *tre = getenv("GWA_TRACE_READ");
-      int traceRead = tre ? atoi(tre) : -1;
-      if (traceRead >= 0 && !d_trace) { HIPCHK(hipMalloc(&d_trace, 4 * 65540)); HIPCHK(hipMemset(d_trace, 0, 4 * 65540)); }
+      const OutSlots os = outSlots(b);
 #ifdef GWA_PROF
       if (sf) throw std::runtime_error("the profiling build times -m bsf only");
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
-                   b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+                   ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
                    (uint32_t *)d_prof, -1);
       {
         std::vector<uint64_t> pv((size_t)lanes * PR_N);
@@ -546,37 +763,44 @@ int gwa_batch_run(gwa_batch_t *b) {
       }
 #else
       if (sf)
-        launchSfSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv, t == 0 ? b->d_all : b->d_list[cur], n,
-                       ix->scratch, stride, caps, b->d_oh, b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank,
-                       b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s);
+        launchSfSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv,
+                       (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh, os,
+                       ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s);
       else
-        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh,
-                     b->d_hits, b->d_cig, b->hitCap, b->cigCap, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
-                     traceRead >= 0 ? d_trace : nullptr, traceRead);
+        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+                     ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1],
+                     ovfCount, s);
 #endif
-      if (traceRead >= 0) {
-        std::vector<uint32_t> tv(65537);
-        HIPCHK(hipMemcpyAsync(tv.data(), d_trace, 4 * 65537, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        FILE *tf = fopen(getenv("GWA_TRACE_FILE") ? getenv("GWA_TRACE_FILE") : "gwa_trace.bin", "wb");
-        if (tf) { fwrite(tv.data(), 4, 1 + tv[0], tf); fclose(tf); }
-      }
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(e2, s));
-      uint32_t nOvf = 0;
-      HIPCHK(hipMemcpyAsync(&nOvf, ovfCount, 4, hipMemcpyDeviceToHost, s));
+      uint32_t ctr[16];
+      HIPCHK(hipMemcpyAsync(ctr, b->d_count, sizeof(ctr), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, e1, e2));
       searchMs += ms;
-      b->stats.tier_reads[t] = n;
-      b->stats.tier_ms[t] = ms;
-      n = nOvf;
+      b->stats.tier_reads[t] += n;
+      b->stats.tier_ms[t] += ms;
+      n = ctr[1 + t];
       cur ^= 1;
+      if (n > 0) {  // the reads rerun on the next tier (instrumentation, gwa_batch_read_counters)
+        std::vector<uint32_t> ids(n);
+        HIPCHK(hipMemcpyAsync(ids.data(), b->d_list[cur], n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const int nt = std::min(t + 1, kNumTiers - 1);
+        for (uint32_t r : ids) b->deep.push_back({r, nt});
+      }
+      b->poolUsedH = std::min<uint64_t>(ctr[12], b->poolHits);
+      b->poolUsedC = std::min<uint64_t>(ctr[13], b->poolCig);
+      const bool refused = ctr[14] > 0;
+      if (refused) {  // reads whose reported hits did not fit the pool: grow it, rerun them
+        if (++regrow > 8) break;
+        growPool(b, ctr[12], ctr[13], s);
+        HIPCHK(hipMemsetAsync(b->d_count + 14, 0, 4, s));
+      }
+      if (t + 1 < kNumTiers) ++t;
+      else if (!refused) break;
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
     b->stats.search_ms = searchMs;
     b->stats.kernel_ms = qms + searchMs;
     if (n > 0) throw std::runtime_error(std::to_string(n) + " reads exceeded the largest search tier");
@@ -593,11 +817,13 @@ int gwa_batch_stats(const gwa_batch_t *b, gwa_batch_stats_t *st) {
 }
 
 static int fetch(gwa_batch *b) {
+  if (b->fetched || b->headerOnly) return 0;
   const uint32_t n = b->n;
   b->oh.resize(n);
-  b->hits.resize((size_t)n * b->hitCap);
-  b->cig.resize((size_t)n * b->cigCap);
-  hipStream_t s = b->ix->stream;
+  b->hits.resize((size_t)n * b->hitCap + b->poolUsedH);
+  b->cig.resize((size_t)n * b->cigCap + b->poolUsedC);
+  HIPCHK(hipSetDevice(b->ix->device));
+  hipStream_t s = b->stream;
   HIPCHK(hipMemcpyAsync(b->oh.data(), b->d_oh, n * sizeof(OutHeader), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(b->hits.data(), b->d_hits, b->hits.size() * sizeof(OutHit), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(b->cig.data(), b->d_cig, b->cig.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
@@ -606,6 +832,7 @@ static int fetch(gwa_batch *b) {
   st.fm_searches = st.quick_steps = st.blocks = st.states = st.quick_blocks = st.sa_reads = st.kmer_lookups = 0;
   st.quick_short_steps = st.quick_sa_reads = st.search_short_steps = 0;
   st.n_mapped = st.n_unmapped = 0;
+  st.num_sw = st.verify_bytes = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const OutHeader &h = b->oh[i];
     st.fm_searches += (uint64_t)h.fmSearches;
@@ -618,82 +845,111 @@ static int fetch(gwa_batch *b) {
     st.quick_short_steps += (uint64_t)h.quickShort;
     st.search_short_steps += (uint64_t)h.searchShort;
     st.states += (uint64_t)h.states;
+    st.num_sw += (uint64_t)h.numSW;
+    st.verify_bytes += (uint64_t)h.verifyBytes;
     if (h.status == ST_MAPPED) st.n_mapped++;
     else if (h.status == ST_UNMAPPED) st.n_unmapped++;
   }
+  b->fetched = true;
   return 0;
 }
+
+}  // extern "C"
+
+// SAM text of the reads idx(0), ..., idx(count - 1), formatted on up to 16 host threads
+template <class Idx>
+static void formatSelected(gwa_batch *b, Idx idx, uint32_t count, gwa_results_t *out) {
+  if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
+  fetch(b);
+  const uint32_t n = count;
+  if (b->headerOnly) {
+    out->n_reads = n;
+    out->sam = (char *)calloc(1, 1);
+    out->sam_len = 0;
+    out->line_off = (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t));
+    return;
+  }
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint32_t i = idx(j);
+    int stt = b->oh[i].status;
+    if (stt == ST_ERROR || stt == ST_OVERFLOW || stt == ST_TOO_LONG) {
+      std::string nm(b->names.data() + (b->nameOff[i] - b->nameOff[0]), b->nameOff[i + 1] - b->nameOff[i]);
+      throw std::runtime_error(std::string(stt == ST_ERROR ? "reference would abort (exception) at read "
+                                                           : stt == ST_TOO_LONG ? "read longer than the device path supports: "
+                                                                                : "output slot overflow at read ") + nm);
+    }
+  }
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::string> parts(nt);
+  std::vector<std::vector<uint64_t>> lens(nt);
+  std::atomic<int> bad{-1};
+  auto work = [&](unsigned t) {
+    uint32_t a = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
+    std::string &o = parts[t];
+    o.reserve((size_t)(e - a) * 320);
+    for (uint32_t j = a; j < e; ++j) {
+      const uint32_t i = idx(j);
+      size_t before = o.size();
+      ReadText rt;
+      rt.name = b->names.data() + (b->nameOff[i] - b->nameOff[0]);
+      rt.nameLen = b->nameOff[i + 1] - b->nameOff[i];
+      rt.seq = b->seqs.data() + (b->seqOff[i] - b->seqOff[0]);
+      rt.seqLen = b->seqOff[i + 1] - b->seqOff[i];
+      if (b->hasQual) {
+        rt.qual = b->quals.data() + (b->qualOff[i] - b->qualOff[0]);
+        rt.qualLen = b->qualOff[i + 1] - b->qualOff[i];
+      } else {
+        rt.qual = nullptr;
+        rt.qualLen = 0;
+      }
+      const OutHeader &h = b->oh[i];
+      if (h.status == ST_MAPPED) {
+        if (formatRead(b->ix->host, rt, h, b->hits.data(), b->cig.data(), o) != 0) bad = (int)i;
+      } else {
+        formatUnmapped(rt, o);
+      }
+      lens[t].push_back(o.size() - before);
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, t);
+  for (auto &x : th) x.join();
+  if (bad >= 0) throw std::runtime_error("reference would abort (exception in AlignmentRecord.convert) at read index " + std::to_string(bad.load()));
+  size_t total = 0;
+  for (auto &p : parts) total += p.size();
+  out->n_reads = n;
+  out->sam = (char *)malloc(total + 1);
+  out->sam_len = total;
+  out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+  size_t pos = 0;
+  uint32_t ri = 0;
+  for (unsigned t = 0; t < nt; ++t) {
+    memcpy(out->sam + pos, parts[t].data(), parts[t].size());
+    for (uint64_t L : lens[t]) { out->line_off[ri++] = pos; pos += L; }
+  }
+  out->line_off[n] = pos;
+  out->sam[total] = 0;
+}
+
+extern "C" {
 
 int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) { return gwa_batch_results_range(b, 0, b->n, out); }
 
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out) {
   try {
-    if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
     if ((uint64_t)first + count > b->n) throw std::runtime_error("result range out of bounds");
-    fetch(b);
-    const uint32_t n = count;
-    for (uint32_t i = first; i < first + n; ++i) {
-      int stt = b->oh[i].status;
-      if (stt == ST_ERROR || stt == ST_OVERFLOW || stt == ST_TOO_LONG) {
-        std::string nm(b->names.data() + (b->nameOff[i] - b->nameOff[0]), b->nameOff[i + 1] - b->nameOff[i]);
-        throw std::runtime_error(std::string(stt == ST_ERROR ? "reference would abort (exception) at read "
-                                                             : stt == ST_TOO_LONG ? "read longer than 255 bases: "
-                                                                                  : "output slot overflow at read ") + nm);
-      }
-    }
-    // SAM formatting in parallel chunks, concatenated in input order
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::string> parts(nt);
-    std::vector<std::vector<uint64_t>> lens(nt);
-    std::atomic<int> bad{-1};
-    auto work = [&](unsigned t) {
-      uint32_t a = first + (uint32_t)((uint64_t)n * t / nt), e = first + (uint32_t)((uint64_t)n * (t + 1) / nt);
-      std::string &o = parts[t];
-      o.reserve((size_t)(e - a) * 320);
-      for (uint32_t i = a; i < e; ++i) {
-        size_t before = o.size();
-        ReadText rt;
-        rt.name = b->names.data() + (b->nameOff[i] - b->nameOff[0]);
-        rt.nameLen = b->nameOff[i + 1] - b->nameOff[i];
-        rt.seq = b->seqs.data() + (b->seqOff[i] - b->seqOff[0]);
-        rt.seqLen = b->seqOff[i + 1] - b->seqOff[i];
-        if (b->hasQual) {
-          rt.qual = b->quals.data() + (b->qualOff[i] - b->qualOff[0]);
-          rt.qualLen = b->qualOff[i + 1] - b->qualOff[i];
-        } else {
-          rt.qual = nullptr;
-          rt.qualLen = 0;
-        }
-        const OutHeader &h = b->oh[i];
-        if (h.status == ST_MAPPED) {
-          for (int c = 0; c < h.nChains; ++c)
-            if (formatChain(b->ix->host, rt, b->hits.data() + (size_t)i * b->hitCap, b->cig.data() + (size_t)i * b->cigCap,
-                            h.chainHead[c], o) != 0)
-              bad = (int)i;
-        } else {
-          formatUnmapped(rt, o);
-        }
-        lens[t].push_back(o.size() - before);
-      }
-    };
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, t);
-    for (auto &x : th) x.join();
-    if (bad >= 0) throw std::runtime_error("reference would abort (exception in AlignmentRecord.convert) at read index " + std::to_string(bad.load()));
-    size_t total = 0;
-    for (auto &p : parts) total += p.size();
-    out->n_reads = n;
-    out->sam = (char *)malloc(total + 1);
-    out->sam_len = total;
-    out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
-    size_t pos = 0;
-    uint32_t ri = 0;
-    for (unsigned t = 0; t < nt; ++t) {
-      memcpy(out->sam + pos, parts[t].data(), parts[t].size());
-      for (uint64_t L : lens[t]) { out->line_off[ri++] = pos; pos += L; }
-    }
-    out->line_off[n] = pos;
-    out->sam[total] = 0;
+    formatSelected(b, [first](uint32_t j) { return first + j; }, count, out);
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
+
+int gwa_batch_results_select(gwa_batch_t *b, const uint32_t *idx, uint32_t count, gwa_results_t *out) {
+  try {
+    for (uint32_t j = 0; j < count; ++j)
+      if (idx[j] >= b->n) throw std::runtime_error("result index out of bounds");
+    formatSelected(b, [idx](uint32_t j) { return idx[j]; }, count, out);
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());
@@ -703,15 +959,23 @@ int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_
 int gwa_batch_read_counters(gwa_batch_t *b, int32_t *out) {
   try {
     if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
+    if (b->headerOnly) throw std::runtime_error("-m bd / -m bwa batches have no device counters");
     fetch(b);
     std::vector<ScanRes> sr(b->n);
     HIPCHK(hipMemcpy(sr.data(), b->d_sres, b->n * sizeof(ScanRes), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < b->n; ++i) {
       const OutHeader &h = b->oh[i];
-      int32_t *o = out + (size_t)i * 12;
+      int32_t *o = out + (size_t)i * GWA_READ_COUNTERS;
       o[8] = sr[i].nmF; o[9] = sr[i].lmF; o[10] = sr[i].nmR; o[11] = sr[i].lmR;
       o[0] = h.status; o[1] = h.fmSearches; o[2] = h.quickSteps; o[3] = h.blocks; o[4] = h.searchBlocks;
       o[5] = h.states; o[6] = h.saReads; o[7] = h.nHits;
+      o[12] = (b->cfg.strategy == 0 && h.states == 0) ? -1 : 0;
+      o[13] = h.kmerLookups; o[14] = h.quickShort; o[15] = h.searchShort;
+      o[16] = h.numSW; o[17] = h.verifyBytes; o[18] = o[19] = 0;
+    }
+    for (auto &d : b->deep) {
+      int32_t &t = out[(size_t)d.first * GWA_READ_COUNTERS + 12];
+      t = std::max(t, (int32_t)d.second);
     }
     return 0;
   } catch (std::exception &e) {

@@ -36,7 +36,7 @@ __device__ __forceinline__ void waveAppend(bool need, uint32_t value, uint32_t *
 
 template <int QW>
 __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
-                                                           OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
+                                                           OutHeader *oh, OutSlots os,
                                                            uint32_t *searchList, uint32_t *searchCount, uint32_t *trace,
                                                            int traceRead) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -46,8 +46,8 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
     const int m = (int)reads.len[r];
     OutHeader *h = oh + r;
     if (m > 32 * QW || m > 255) {
+      *h = OutHeader{};
       h->status = ST_TOO_LONG;
-      h->nChains = h->nHits = h->nCigar = 0;
     } else {
       StairTables st{};
       LaneMem<4> L{};
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
       BsfLane<4, QW> lane(ix, cfg, st, L, caps);
       if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
       lane.initRead(reads.codes + o, m);
-      need = lane.quickPhase(sres + r, h, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap) != 0;
+      need = lane.quickPhase(sres + r, h, os, r) != 0;
       if (lane.trace) trace[0] = (uint32_t)lane.traceN;
     }
   }
@@ -68,8 +68,8 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
 template <int R, int QW, int LH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES))) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
                                                          const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
-                                                         uint64_t laneStride, Caps caps, OutHeader *oh, OutHit *ohits,
-                                                         uint16_t *ocig, int hitCap, int cigCap, const int32_t *chrRank,
+                                                         uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
+                                                         const int32_t *chrRank,
                                                          uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *trace,
                                                          int traceRead) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
         if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
         lane.initRead(reads.codes + o, m);
         lane.searchPhase(sres[r]);
-        lane.writeSearchOutput(oh + r, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap, hitCap, cigCap);
+        lane.writeSearchOutput(oh + r, os, r);
         if (lane.trace) trace[0] = (uint32_t)lane.traceN;
         ovf = oh[r].status == ST_OVERFLOW;
       }
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
     }
     bool ovf = false;
     if (phase == FINISH) {
-      lane.writeSearchOutput(oh + r, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap, hitCap, cigCap);
+      lane.writeSearchOutput(oh + r, os, r);
       if (lane.trace) trace[0] = (uint32_t)lane.traceN;
       ovf = oh[r].status == ST_OVERFLOW;
       phase = IDLE;
@@ -196,8 +196,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 template <int R, int QW>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES)))
 sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
-                 uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig,
-                 int hitCap, int cigCap, const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount) {
+                 uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
+                 const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
   uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
@@ -238,7 +238,7 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
     } else {
       lane.initRead(reads.codes + reads.off[r], m);
       lane.sfSearch();
-      lane.writeSearchOutput(h, ohits + (size_t)r * hitCap, ocig + (size_t)r * cigCap, hitCap, cigCap);
+      lane.writeSearchOutput(h, os, r);
       h->quickSteps = lane.quickSteps;
       h->blocks = 0;  // (all Occ blocks are in searchBlocks on this path)
       h->kmerLookups = lane.kmerLookups;
@@ -263,22 +263,22 @@ void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream
 }
 
 void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                     OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap, uint32_t *searchList, uint32_t *searchCount,
+                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace, int traceRead) {
   if (reads.n == 0) return;
   dim3 grid((reads.n + 255) / 256);
   if (QW == 4)
-    hipLaunchKernelGGL(fm_quickscan_kernel<4>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, ohits, ocig, hitCap, cigCap,
+    hipLaunchKernelGGL(fm_quickscan_kernel<4>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
                        searchList, searchCount, trace, traceRead);
   else
-    hipLaunchKernelGGL(fm_quickscan_kernel<8>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, ohits, ocig, hitCap, cigCap,
+    hipLaunchKernelGGL(fm_quickscan_kernel<8>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
                        searchList, searchCount, trace, traceRead);
 }
 
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,
                   const StairTables &st, const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n,
-                  uint8_t *scratch, uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig,
-                  int hitCap, int cigCap, const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
+                  uint8_t *scratch, uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,
+                  const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
                   hipStream_t s, uint32_t *trace, int traceRead) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
@@ -287,7 +287,7 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
 #define GWA_CASE(RR, QQ, LL)                                                                                          \
   case (RR * 16 + QQ) * 2 + LL:                                                                                       \
     hipLaunchKernelGGL((bsf_search_kernel<RR, QQ, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
-                       scratch, laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, work, ovfList, ovfCount,  \
+                       scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount,                          \
                        trace, traceRead);                                                                             \
     break;
 #define GWA_CASE2(RR, QQ) GWA_CASE(RR, QQ, 0) GWA_CASE(RR, QQ, 1)
@@ -307,7 +307,7 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
 
 void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
-                    const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
+                    const Caps &caps, OutHeader *oh, const OutSlots &os,
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
@@ -315,7 +315,7 @@ void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const Se
 #define GWA_SF(RR, QQ)                                                                                               \
   case RR * 16 + QQ:                                                                                                 \
     hipLaunchKernelGGL((sf_search_kernel<RR, QQ>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,      \
-                       laneStride, caps, oh, ohits, ocig, hitCap, cigCap, chrRank, work, ovfList, ovfCount);       \
+                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount);                                  \
     break;
     GWA_SF(4, 4)
     GWA_SF(4, 8)

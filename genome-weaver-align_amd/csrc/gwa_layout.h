@@ -121,23 +121,53 @@ struct OutHit {           // one ReadHit (R/ReadHit.java:42-53)
   int32_t matchLength, qStart, qEnd, diff;
   int32_t strand, numHits;
   int32_t next;           // index of nextSplit within the record's hits, -1 = none
-  uint16_t cigarOff, cigarLen;
+  uint32_t cigarOff, cigarLen;  // ops [cigarOff, cigarOff + cigarLen) of the record's CIGAR area
 };
 
-// Fixed-size per-read output slot.
+// Per-read output header.  A read's hits are OutHit[hitOff, hitOff + nHits) and its CIGAR ops
+// cig[cigOff, cigOff + nCigar); the reported chains lie back to back in report order (chain c + 1
+// starts after the last hit of chain c), so no per-chain index is stored and the number of reported
+// chains is not bounded (-R allhits reports every hit, S/BidirectionalSuffixFilter.java:240-255).
 struct OutHeader {
   int32_t status;
   int32_t nChains;   // reported ReadHit chains (BESTHIT: 1)
   int32_t nHits;     // OutHit entries used
   int32_t nCigar;    // cigar ops used
-  int32_t chainHead[4];
+  uint32_t hitOff, cigOff;
+  int32_t poolFail;  // 1: ST_OVERFLOW came from a full output pool, not from a search capacity
+  int32_t numSW;     // DP verifications (alignBlockDetailed calls, the reference's numSW)
   // instrumentation: FM steps, quick-scan steps, rank block loads
   int32_t fmSearches, quickSteps, blocks, states;
   int32_t searchBlocks, saReads, maxHeap, kmerLookups;  // maxHeap: heap high-water mark (instrumentation)
   // quick-scan steps answered without Occ blocks (k-mer table or single-row text compare)
-  int32_t quickShort, quickSa, searchShort, pad_;  // quickSa: SA gathers of the quick scan; searchShort:
+  int32_t quickShort, quickSa, searchShort;  // quickSa: SA gathers of the quick scan; searchShort:
   // search FM steps answered by one text character (M_TEXT)
+  int32_t verifyBytes;  // SURVEY.md §8d verify bytes: ceil(2n/8) + ceil(n/8) of each n-base window + 32 B Peq per block
 };
+
+// Where reads write their reported hits: read r owns the fixed slot hits[r * hitCap, + hitCap) and
+// cig[r * cigCap, + cigCap); a read reporting more (-R allhits / topL with many equal hits, long
+// split chains) reserves room in the shared pool behind the slots with one atomic bump per array.
+// A reservation past the pool end marks the read ST_OVERFLOW with poolFail = 1; the host grows the
+// pool and reruns it (gwa_batch_run).
+struct OutSlots {
+  OutHit *hits;
+  uint16_t *cig;
+  uint32_t hitCap, cigCap;
+  uint32_t *poolUsed;            // [0] hits, [1] cigar ops reserved so far, [2] reads refused
+  uint64_t poolHit0, poolHitEnd; // pool = hits[poolHit0, poolHitEnd)
+  uint64_t poolCig0, poolCigEnd; //        cig[poolCig0, poolCigEnd)
+};
+
+GWA_HD uint32_t outReserve(uint32_t *ctr, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicAdd(ctr, v);
+#else
+  const uint32_t o = *ctr;  // host replay (tests/hostcore) is one read at a time
+  *ctr = o + v;
+  return o;
+#endif
+}
 
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at
 // S/BidirectionalSuffixFilter.java:324-346)

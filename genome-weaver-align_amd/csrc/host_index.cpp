@@ -12,12 +12,6 @@
 
 namespace gwa {
 
-static std::string trimJ(const char *a, const char *b) {
-  while (a < b && (unsigned char)*a <= ' ') a++;
-  while (b > a && (unsigned char)b[-1] <= ' ') b--;
-  return std::string(a, b);
-}
-
 void addSequence(const std::string &name, const char *seq, size_t len, HostIndex &ix) {
   int64_t off = (int64_t)ix.T.size();
   for (size_t i = 0; i < len; ++i)
@@ -29,16 +23,22 @@ void addSequence(const std::string &name, const char *seq, size_t len, HostIndex
 }
 
 void packFasta(const char *text, size_t len, HostIndex &ix) {
+  // one pass, lines found with memchr, codes written through a 256-entry table
+  uint8_t lut[256];
+  for (int c = 0; c < 256; ++c) lut[c] = to3bit((unsigned char)c);
   const char *p = text, *end = text + len;
   bool inSeq = false;
   std::string name;
   int64_t off = (int64_t)ix.T.size();
+  size_t n = ix.T.size();
+  ix.T.resize(n + len);  // upper bound, trimmed at the end
+  uint8_t *o = ix.T.data();
   auto finish = [&]() {
     if (!inSeq) return;
     ix.names.push_back(name);
     ix.offsets.push_back(off);
-    ix.lengths.push_back((int64_t)ix.T.size() - off);
-    off = (int64_t)ix.T.size();
+    ix.lengths.push_back((int64_t)n - off);
+    off = (int64_t)n;
   };
   while (p < end) {
     const char *e = (const char *)memchr(p, '\n', (size_t)(end - p));
@@ -54,13 +54,17 @@ void packFasta(const char *text, size_t len, HostIndex &ix) {
       name.assign(a, b);
       inSeq = true;
     } else if (inSeq) {
-      std::string t = trimJ(p, le);
-      for (char c : t) ix.T.push_back(to3bit((unsigned char)c));
+      // the line trimmed of chars <= ' ' at both ends (Java String.trim), every char through to3bit
+      const char *a = p, *b = le;
+      while (a < b && (unsigned char)*a <= ' ') a++;
+      while (b > a && (unsigned char)b[-1] <= ' ') b--;
+      for (; a < b; ++a) o[n++] = lut[(unsigned char)*a];
     }
     p = e + 1;
   }
   finish();
-  ix.N = ix.T.size();
+  ix.T.resize(n);
+  ix.N = n;
 }
 
 void rankNames(HostIndex &ix) {

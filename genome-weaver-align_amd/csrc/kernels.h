@@ -11,16 +11,16 @@ namespace gwa {
 struct Caps;
 
 void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                     OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap, uint32_t *searchList, uint32_t *searchCount,
+                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace = nullptr, int traceRead = -1);
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
-                  uint64_t laneStride, const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
+                  uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,
                   const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s,
                   uint32_t *trace = nullptr, int traceRead = -1);
 void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
-                    const Caps &caps, OutHeader *oh, OutHit *ohits, uint16_t *ocig, int hitCap, int cigCap,
+                    const Caps &caps, OutHeader *oh, const OutSlots &os,
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s);
 void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream_t s);
 size_t laneBytesFor(int R, const Caps &c);  // per-lane slice

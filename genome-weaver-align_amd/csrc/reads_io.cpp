@@ -40,8 +40,10 @@ struct Lines {
   bool final;
   bool next(uint64_t *b, uint64_t *e) {
     if (pos >= len) return false;
-    uint64_t i = pos;
-    while (i < len && t[i] != '\n' && t[i] != '\r') ++i;
+    // the next "\n" (memchr), unless a "\r" comes first
+    const char *nl = (const char *)memchr(t + pos, '\n', len - pos);
+    uint64_t i = nl ? (uint64_t)(nl - t) : len;
+    if (const char *cr = (const char *)memchr(t + pos, '\r', i - pos)) i = (uint64_t)(cr - t);
     if (i == len) {
       if (!final) return false;
       *b = pos; *e = len; pos = len;
@@ -140,6 +142,46 @@ uint64_t parseFastq(const char *t, uint64_t len, bool final, Buf &o) {
 }
 
 }  // namespace
+
+namespace gwa {
+// Record framing for the pipeline reader: the end offset of the first `maxRec` complete records of
+// text[0, len) (fewer when the text ends first) under the same rules as parseFasta / parseFastq, and
+// their count.  Only line ends are scanned (memchr); the parse itself runs later, in parallel, on each
+// framed slice.  Malformed records are left to that parse to report.
+uint64_t frameRecords(const char *t, uint64_t len, int format, bool final, uint64_t maxRec, uint64_t *nRec) {
+  Lines L{t, len, 0, final};
+  uint64_t done = 0, n = 0, b, e;
+  if (format == 1) {
+    while (n < maxRec) {
+      const uint64_t recStart = L.pos;
+      if (!L.next(&b, &e)) break;
+      if (e == b) { done = L.pos; continue; }
+      uint64_t x0, x1;
+      const bool ok = L.next(&x0, &x1) && L.next(&x0, &x1) && L.next(&x0, &x1);
+      if (!ok && !final) { L.pos = recStart; break; }
+      ++n;
+      done = L.pos;
+    }
+  } else {
+    bool inRec = false;
+    while (true) {
+      const uint64_t lineStart = L.pos;
+      if (!L.next(&b, &e)) break;
+      if (e > b && t[b] == '>') {
+        if (inRec && ++n == maxRec) { done = lineStart; inRec = false; break; }
+        inRec = true;
+        done = lineStart;
+      } else if (!inRec) {
+        done = L.pos;
+      }
+    }
+    if (inRec && final) { ++n; done = len; }
+    if (!inRec && n < maxRec && final) done = len;
+  }
+  *nRec = n;
+  return done;
+}
+}  // namespace gwa
 
 extern "C" int gwa_fail_message(const char *msg);  // gwa_api.cpp: sets gwa_last_error, returns -1
 

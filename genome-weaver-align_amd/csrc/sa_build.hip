@@ -140,6 +140,32 @@ __global__ void packText(const uint8_t *__restrict__ T, uint64_t N, uint64_t *__
   }
 }
 
+// inverse of packText: codes 0..4 from the 2-bit text + N bitmap (a saved index, gwa_index_save)
+__global__ void unpackText(const uint64_t *__restrict__ text2, const uint64_t *__restrict__ textN, uint64_t N,
+                           uint8_t *__restrict__ T) {
+  for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < N; p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t w = text2[p >> 5];
+    const uint8_t c = (uint8_t)((w >> (2 * (p & 31))) & 3);
+    T[p] = ((textN[p >> 6] >> (p & 63)) & 1) ? (uint8_t)4 : c;
+  }
+}
+
+// CharacterCount (A/CharacterCount.java:41-50): occurrences of codes 0..4, one atomic per workgroup
+// and code
+__global__ void countCodes(const uint8_t *__restrict__ T, uint64_t N, unsigned long long *__restrict__ cnt) {
+  __shared__ unsigned long long c[5];
+  if (threadIdx.x < 5) c[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long m[5] = {0, 0, 0, 0, 0};
+  for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < N; p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint8_t x = T[p];
+    m[x > 4 ? 4 : x]++;
+  }
+  for (int i = 0; i < 5; ++i) atomicAdd(&c[i], m[i]);
+  __syncthreads();
+  if (threadIdx.x < 5) atomicAdd(&cnt[threadIdx.x], c[threadIdx.x]);
+}
+
 // Cyclic suffix array of d_T[0,N) into d_sa (both device).  alphabetBits 3 for codes 0..4.
 // Returns false when the text is periodic (rotations tie).
 bool cyclicSAGpu(const uint8_t *d_T, uint64_t N, uint32_t *d_sa, int alphabetBits, hipStream_t s) {
@@ -226,6 +252,19 @@ void buildOccGpu(const uint8_t *d_T, const uint32_t *d_sa, uint64_t N, OccBlock 
   SCHK(hipStreamSynchronize(s));
   (void)hipFree(tmp);
   (void)hipFree(local);
+}
+
+void unpackTextGpu(const uint64_t *d_text2, const uint64_t *d_textN, uint64_t N, uint8_t *d_T, hipStream_t s) {
+  const unsigned g = gridFor(N);
+  hipLaunchKernelGGL(unpackText, dim3(g > 65536 ? 65536 : g), dim3(256), 0, s, d_text2, d_textN, N, d_T);
+  SCHK(hipGetLastError());
+}
+
+void countCodesGpu(const uint8_t *d_T, uint64_t N, unsigned long long *d_cnt5, hipStream_t s) {
+  SCHK(hipMemsetAsync(d_cnt5, 0, 5 * sizeof(unsigned long long), s));
+  const unsigned g = gridFor(N);
+  hipLaunchKernelGGL(countCodes, dim3(g > 4096 ? 4096 : g), dim3(256), 0, s, d_T, N, d_cnt5);
+  SCHK(hipGetLastError());
 }
 
 void packTextGpu(const uint8_t *d_T, uint64_t N, uint64_t *d_text2, uint64_t *d_textN, hipStream_t s) {

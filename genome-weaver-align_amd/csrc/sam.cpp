@@ -174,10 +174,9 @@ int formatChain(const HostIndex &ix, const ReadText &rt, const OutHit *hits, con
     rec.cigar = cigOf(h); rec.seq = query; rec.qualNull = qualNull; rec.qual = qual; rec.numBestHits = h.numHits;
     rec.state = st;
   } else {
+    // the head and its first split are converted; later fragments of a longer chain are dropped
+    // (R/AlignmentRecord.java:201-206 reads hit.nextSplit only), but still named in XP (chainState)
     const OutHit &s = hits[h.next];
-    if (s.next >= 0) return -1;  // only two-fragment chains are converted (TODO in the reference, :206)
-    int totalDiff = h.diff + 1 + s.diff;
-    (void)totalDiff;
     const int numHits = h.numHits;
     int qualLen = !qualNull ? (int)qual.size() : h.matchLength;
     auto sub = [&](const std::string &x, int a, int b) -> std::string {
@@ -241,6 +240,20 @@ int formatChain(const HostIndex &ix, const ReadText &rt, const OutHit *hits, con
   line(cx, rec, rec.split != nullptr, true, true, out, &npe);
   out += '\n';
   return npe ? -1 : 0;
+}
+
+int formatRead(const HostIndex &ix, const ReadText &rt, const OutHeader &h, const OutHit *hits, const uint16_t *cig,
+               std::string &out) {
+  const OutHit *hb = hits + h.hitOff;
+  const uint16_t *cb = cig + h.cigOff;
+  int head = 0;
+  for (int c = 0; c < h.nChains; ++c) {
+    if (formatChain(ix, rt, hb, cb, head, out) != 0) return -1;
+    int t = head;
+    while (hb[t].next >= 0) t = hb[t].next;
+    head = t + 1;
+  }
+  return 0;
 }
 
 // The unmapped record: ReadHit("*", 0, 0, 0, 0, -1, FORWARD, CIGAR(), 0) (S/BidirectionalSuffixFilter.java:258-261)

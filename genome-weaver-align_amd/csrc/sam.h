@@ -18,5 +18,9 @@ struct ReadText {
 std::string samHeader(const HostIndex &ix);
 int formatChain(const HostIndex &ix, const ReadText &rt, const OutHit *hits, const uint16_t *cig, int head, std::string &out);
 void formatUnmapped(const ReadText &rt, std::string &out);
+// every reported chain of a mapped read (OutHeader: hits and CIGAR ops at hitOff / cigOff, chains
+// back to back); 0, or -1 where the reference would throw
+int formatRead(const HostIndex &ix, const ReadText &rt, const OutHeader &h, const OutHit *hits, const uint16_t *cig,
+               std::string &out);
 
 }  // namespace gwa

@@ -35,6 +35,25 @@ def max_over_ranks(value):
     return float(t[0])
 
 
+def all_gather_floats(value):
+    """[value of rank 0, value of rank 1, ...] on every rank; [value] when not distributed."""
+    import torch
+    import torch.distributed as td
+    if not (td.is_available() and td.is_initialized()) or td.get_world_size() == 1:
+        return [float(value)]
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(td.get_world_size())]
+    td.all_gather(out, torch.tensor([float(value)], dtype=torch.float64))
+    return [float(t[0]) for t in out]
+
+
+def device_for(local_rank, n_devices):
+    """GPU ordinal of a local rank: ranks beyond the node's GPU count share GPUs round-robin (so a
+    2-rank run works on a 1-GPU box, each rank holding its own index replica)."""
+    if n_devices < 1:
+        raise RuntimeError("no GPU visible")
+    return local_rank % n_devices
+
+
 def gather_sam(sam_text, dst=0):
     """Gather each rank's SAM text to `dst`, concatenated in rank order (None on other ranks)."""
     import torch.distributed as td

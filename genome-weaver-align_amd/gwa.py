@@ -46,17 +46,25 @@ class BatchStats(ctypes.Structure):
                 ("quick_blocks", ctypes.c_uint64), ("states", ctypes.c_uint64), ("sa_reads", ctypes.c_uint64), ("tier_reads", ctypes.c_uint32 * 4),
                 ("n_mapped", ctypes.c_uint32), ("n_unmapped", ctypes.c_uint32), ("kmer_lookups", ctypes.c_uint64),
                 ("quick_short_steps", ctypes.c_uint64), ("quick_sa_reads", ctypes.c_uint64),
-                ("search_short_steps", ctypes.c_uint64), ("tier_ms", ctypes.c_float * 4)]
+                ("search_short_steps", ctypes.c_uint64), ("tier_ms", ctypes.c_float * 4),
+                ("num_sw", ctypes.c_uint64), ("verify_bytes", ctypes.c_uint64)]
+
+
+class PipelineStats(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_uint64), ("batches", ctypes.c_uint64), ("wall_s", ctypes.c_double),
+                ("read_s", ctypes.c_double), ("device_kernel_s", ctypes.c_double * 16)]
 
 
 _lib = None
 
 # every symbol include/gwa.h declares (checked by tests/test_cabi.py)
 EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_index_build_fasta", "gwa_index_open",
-           "gwa_index_build_codes", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
+           "gwa_index_build_codes", "gwa_index_save", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
            "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
            "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
-           "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_reads_parse", "gwa_reads_free"]
+           "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_batch_results_select",
+           "gwa_pipeline_open", "gwa_pipeline_align", "gwa_pipeline_align_file", "gwa_pipeline_stats",
+           "gwa_pipeline_close", "gwa_reads_parse", "gwa_reads_free"]
 
 
 def lib():
@@ -71,6 +79,7 @@ def lib():
         L.gwa_index_build_fasta.argtypes = [ctypes.c_char_p, U64, I, P(V)]
         L.gwa_index_open.argtypes = [ctypes.c_char_p, I, P(V)]
         L.gwa_index_build_codes.argtypes = [V, U64, ctypes.c_int32, V, V, I, P(V)]
+        L.gwa_index_save.argtypes = [V, ctypes.c_char_p]
         L.gwa_index_text_size.restype = U64
         L.gwa_index_text_size.argtypes = [V]
         L.gwa_index_device_bytes.restype = U64
@@ -88,8 +97,14 @@ def lib():
         L.gwa_batch_free.argtypes = [V]
         L.gwa_batch_read_counters.argtypes = [V, V]
         L.gwa_batch_results_range.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, P(_Results)]
+        L.gwa_batch_results_select.argtypes = [V, V, ctypes.c_uint32, P(_Results)]
         L.gwa_reads_parse.argtypes = [ctypes.c_char_p, U64, I, I, P(_ReadBuf), P(U64)]
         L.gwa_reads_free.argtypes = [P(_ReadBuf)]
+        L.gwa_pipeline_open.argtypes = [V, I, P(_Config), ctypes.c_uint32, I, P(V)]
+        L.gwa_pipeline_align.argtypes = [V, P(_Reads), P(_Results)]
+        L.gwa_pipeline_align_file.argtypes = [V, ctypes.c_char_p, I, P(U64)]
+        L.gwa_pipeline_stats.argtypes = [V, P(PipelineStats)]
+        L.gwa_pipeline_close.argtypes = [V]
         _lib = L
     return _lib
 
@@ -99,7 +114,7 @@ def _check(rc):
         raise GwaError(lib().gwa_last_error().decode())
 
 
-STRATEGIES = {"bsf": 0, "sf": 1}
+STRATEGIES = {"bsf": 0, "sf": 1, "bd": 2, "bwa": 3}
 REPORT_TYPES = {"besthit": 0, "allhits": 1, "topl": 2}
 
 
@@ -186,6 +201,10 @@ class FMIndexOnGenome:
         _check(lib().gwa_index_build_codes(codes.ctypes.data, len(codes), len(names), ctypes.cast(arr, ctypes.c_void_p),
                                           ln.ctypes.data, device, ctypes.byref(h)))
         return cls(h, device)
+
+    def save(self, path):
+        """Write the index (gwa_index_save); FMIndexOnGenome.load(path) reads it back without the FASTA."""
+        _check(lib().gwa_index_save(self.h, path.encode()))
 
     def textSize(self):
         return lib().gwa_index_text_size(self.h)
@@ -342,6 +361,12 @@ class SuffixFilter(BidirectionalSuffixFilter):
         super().__init__(fmIndex, dataclasses.replace(config or AlignmentConfig(), strategy="sf"))
 
 
+class BidirectionalBWT(BidirectionalSuffixFilter):
+    """`-m bd` / `-m bwa` (S/BidirectionalBWT.java): the reference reports BWAState / AlignmentSA
+    objects that SAMOutput.emit drops (A/SAMOutput.java:73-82), so its SAM holds the header only;
+    align_batch returns no records, as the reference prints none."""
+
+
 def aligner(fmIndex, config):
     """Align.query's strategy switch (A/Align.java:116-137): the Aligner for config.strategy."""
     s = config.strategy.lower()
@@ -349,7 +374,59 @@ def aligner(fmIndex, config):
         return SuffixFilter(fmIndex, config)
     if s == "bsf":
         return BidirectionalSuffixFilter(fmIndex, config)
-    raise GwaError("%s mode is not supported on the device path" % config.strategy)
+    if s in ("bd", "bwa"):
+        return BidirectionalBWT(fmIndex, config)
+    raise GwaError("%s mode is not supported" % config.strategy)
+
+
+class Pipeline:
+    """Multi-device driver (include/gwa.h gwa_pipeline_*): read batches dealt to several index replicas
+    (one per GPU), SAM in input order.  indexes: FMIndexOnGenome handles, one per device."""
+
+    def __init__(self, indexes, config, batch_reads=1 << 20, workers_per_device=2):
+        self.indexes = list(indexes)
+        arr = (ctypes.c_void_p * len(self.indexes))(*[ix.h.value if hasattr(ix.h, "value") else ix.h
+                                                       for ix in self.indexes])
+        self.config = config
+        self.h = ctypes.c_void_p()
+        c = config._c()
+        _check(lib().gwa_pipeline_open(ctypes.cast(arr, ctypes.c_void_p), len(self.indexes), ctypes.byref(c),
+                                       batch_reads, workers_per_device, ctypes.byref(self.h)))
+
+    def align_batch(self, reads):
+        """reads: list of (name, seq, qual-or-None) -> SAM text (no header), input order."""
+        keep = []
+        r = _reads_struct(reads, keep)
+        res = _Results()
+        _check(lib().gwa_pipeline_align(self.h, ctypes.byref(r), ctypes.byref(res)))
+        return _take_results(res)[0]
+
+    def align_reads(self, reads_struct):
+        res = _Results()
+        _check(lib().gwa_pipeline_align(self.h, ctypes.byref(reads_struct), ctypes.byref(res)))
+        return _take_results(res)[0]
+
+    def align_file(self, path, fd):
+        """Stream a FASTA/FASTQ[.gz] read file through the devices; SAM records to file descriptor fd."""
+        n = ctypes.c_uint64()
+        _check(lib().gwa_pipeline_align_file(self.h, path.encode(), fd, ctypes.byref(n)))
+        return n.value
+
+    def stats(self):
+        st = PipelineStats()
+        _check(lib().gwa_pipeline_stats(self.h, ctypes.byref(st)))
+        return st
+
+    def close(self):
+        if self.h:
+            lib().gwa_pipeline_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def reads_from_blobs(name_blob, name_off, seq_blob, seq_off, qual_blob=None, qual_off=None):
@@ -398,6 +475,14 @@ class Batch:
             _check(lib().gwa_batch_results_range(self.h, first, count, ctypes.byref(res)))
         return _take_results(res)
 
+    def results_select(self, idx):
+        """(SAM text, line offsets) of the reads idx (any order, as given)."""
+        import numpy as np
+        idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        res = _Results()
+        _check(lib().gwa_batch_results_select(self.h, idx.ctypes.data, len(idx), ctypes.byref(res)))
+        return _take_results(res)
+
     def sam_size(self):
         """Format the whole batch's SAM text in the library (D2H of the records + host formatting) and
         return its size in bytes without copying it into Python (host-pipeline timing)."""
@@ -407,11 +492,14 @@ class Batch:
         lib().gwa_results_free(ctypes.byref(res))
         return n
 
+    READ_COUNTERS = 20  # include/gwa.h GWA_READ_COUNTERS
+
     def read_counters(self):
-        """per read: status, fm_searches, quick_steps, quickscan_blocks, search_blocks, states, sa_reads, n_hits"""
+        """per read (include/gwa.h gwa_batch_read_counters): status, fm_searches, quick_steps, quickscan_blocks,
+        search_blocks, states, sa_reads, n_hits, quick-scan mismatches/starts x4, deepest tier, k-mer lookups,
+        quick short steps, search text steps, DP verifications, verify bytes"""
         import numpy as np
-        n = ctypes.c_uint32()
-        out = np.zeros((self.n, 12), dtype=np.int32)
+        out = np.zeros((self.n, self.READ_COUNTERS), dtype=np.int32)
         _check(lib().gwa_batch_read_counters(self.h, out.ctypes.data))
         return out
 

@@ -1,14 +1,18 @@
 """`align` command of genome-weaver on MI355X (A/Align.java:57-110 and the options of
 A/AlignmentConfig.java:40-72, A/AlignmentScoreConfig.java:37-77).
 
+  python genome-weaver-align_amd/gwa_cli.py bwt ref.fa            (writes ref.fa.gwa.idx)
   python genome-weaver-align_amd/gwa_cli.py align -r ref.fa [-q SEQ | reads.fq[.gz] | reads.fa[.gz]]
-         [-k 0.1] [-m bsf|sf] [-R besthit|allhits|topL] [-L 5] [-g 1] [-e 4] [-s 1] [-M 1] [-N 3]
-         [-G 11] [-E 4] [-S 11] [-P 5] [-W 31] [--silent] [--device 0] [--batch 1048576]
+         [-k 0.1] [-m bsf|sf|bd|bwa] [-R besthit|allhits|topL] [-L 5] [-g 1] [-e 4] [-s 1] [-M 1] [-N 3]
+         [-G 11] [-E 4] [-S 11] [-P 5] [-W 31] [--silent] [--devices 0,1,..] [--batch 1048576]
 
 Writes SAM to stdout: the `@SQ` header (SequenceBoundary.toSAMHeader, A/SequenceBoundary.java:81-87)
-then one record per read in input order, as SAMOutput does (A/SAMOutput.java:56-82).  Reads are
-aligned in batches on one GPU; the index is built on the GPU from the FASTA at start-up (the
-reference instead loads the files of its `bwt` command, A/FMIndexOnGenome.java:60-86).
+then one record per read in input order, as SAMOutput does (A/SAMOutput.java:56-82).  Read files go
+through the library's multi-device pipeline (gwa_pipeline_align_file): batches dealt to one index
+replica per GPU in --devices, SAM written back in input order.  Like the reference, which loads the
+files its `bwt` command wrote next to the FASTA (A/FMIndexOnGenome.java:60-86, A/BWTFiles.java:40-80),
+`align -r ref.fa` loads `ref.fa.gwa.idx` when `bwt` made one, and otherwise builds the index on the GPU
+from the FASTA.
 
 Read input follows ReadReaderFactory.createReader (R/ReadReaderFactory.java:126-151): `.fa`,
 `.fasta`, `.fan`, `.fastq`, `.fq`, optionally `.gz`; `-q` aligns one query named "read" with no
@@ -17,8 +21,10 @@ of the header line (utgb FastqReader / FASTAPullParser are unvendored: parity un
 """
 import argparse
 import gzip
+import io
 import os
 import sys
+import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -84,27 +90,6 @@ def reads_of(path):
         f.close()
 
 
-def native_chunks(path, chunk=64 << 20):
-    """The read file as library-parsed chunks (gwa.ParsedReads, include/gwa.h gwa_reads_parse): the
-    host side of the pipeline stays native for large files; read_fasta / read_fastq state the same
-    record rules in Python (tests/test_cli.py holds the two to identical output)."""
-    kind = _kind(path)
-    opener = gzip.open if path.endswith(".gz") else open
-    with opener(path, "rb") as f:
-        carry = b""
-        while True:
-            data = f.read(chunk)
-            final = not data
-            buf = carry + data
-            if not buf:
-                return
-            pr = gwa.ParsedReads(buf, kind, final)
-            yield pr
-            carry = buf[pr.consumed:]
-            if final:
-                return
-
-
 def build_parser():
     ap = argparse.ArgumentParser(prog="gwa", description="genome-weaver read alignment on MI355X")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -113,7 +98,7 @@ def build_parser():
     a.add_argument("-q", dest="query", help="single query sequence")
     a.add_argument("readFiles", nargs="*", help="read file (single-end)")
     a.add_argument("--silent", action="store_true", help="disable output")
-    a.add_argument("-m", dest="strategy", default="bsf", help="alignment strategy: bsf (default), sf")
+    a.add_argument("-m", dest="strategy", default="bsf", help="alignment strategy: bsf (default), sf, bd, bwa")
     a.add_argument("-R", dest="reportType", default="besthit", help="besthit (default), allhits, topL")
     a.add_argument("-L", dest="topL", type=int, default=5)
     a.add_argument("-k", dest="k", type=float, default=0.1,
@@ -128,7 +113,13 @@ def build_parser():
     a.add_argument("-S", dest="splitOpenPenalty", type=int, default=11)
     a.add_argument("-P", dest="indelEndSkip", type=int, default=5)
     a.add_argument("-W", dest="bandWidth", type=int, default=31)
-    a.add_argument("--device", type=int, default=0, help="GPU ordinal")
+    a.add_argument("--device", type=int, default=0, help="GPU ordinal (one device)")
+    a.add_argument("--devices", default=None, help="comma-separated GPU ordinals: one index replica per GPU")
+    a.add_argument("--workers", type=int, default=2, help="host worker threads per device")
+    b = sub.add_parser("bwt", help="build and save the index of a FASTA (loaded by align -r)")
+    b.add_argument("fasta")
+    b.add_argument("-o", dest="out", default=None, help="index file (default: <fasta>.gwa.idx)")
+    b.add_argument("--device", type=int, default=0)
     a.add_argument("--batch", type=int, default=1 << 20, help="reads per device batch")
     a.add_argument("--timing", action="store_true", help="index / align wall times and reads/s on stderr")
     return ap
@@ -145,6 +136,36 @@ def config_of(ns):
     return cfg
 
 
+def index_path(ref):
+    """The saved index the `bwt` command writes for a FASTA (or the path itself when it is one)."""
+    return ref + ".gwa.idx"
+
+
+def load_indexes(ref, devices):
+    """One FMIndexOnGenome per device (built in parallel; each GPU holds a full replica)."""
+    import threading
+    src = index_path(ref) if os.path.exists(index_path(ref)) else ref
+    out, errs = [None] * len(devices), []
+
+    def one(i, d):
+        try:
+            out[i] = gwa.FMIndexOnGenome.load(src, device=d)
+        except gwa.GwaError as e:
+            errs.append(e)
+
+    th = [threading.Thread(target=one, args=(i, d)) for i, d in enumerate(devices)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        for x in out:
+            if x is not None:
+                x.close()
+        raise errs[0]
+    return out
+
+
 def align(ns, out=sys.stdout):
     if ns.query is None and not ns.readFiles:
         raise gwa.GwaError("no query is given")
@@ -153,29 +174,58 @@ def align(ns, out=sys.stdout):
     cfg = config_of(ns)
     if ns.query is None:
         _kind(ns.readFiles[0])  # unsupported suffixes fail before the index is built
+    devices = [int(x) for x in ns.devices.split(",")] if ns.devices else [ns.device]
     t0 = time.perf_counter()
-    fm = gwa.FMIndexOnGenome.load(ns.refSeq, device=ns.device)
+    fms = load_indexes(ns.refSeq, devices)
     t1 = time.perf_counter()
-    bsf = gwa.aligner(fm, cfg)
     w = (lambda s: None) if ns.silent else out.write
-    w(fm.samHeader())
+    w(fms[0].samHeader())
     n = 0
-    if ns.query is not None:
-        w(bsf.align_batch([("read", ns.query, None)]))
-        n = 1
-    else:
-        for pr in native_chunks(ns.readFiles[0]):
-            for i in range(0, pr.n, ns.batch):
-                c = min(ns.batch, pr.n - i)
-                w(gwa.align_reads(bsf, pr.slice(i, c)))
-                n += c
-            pr.close()
+    try:
+        if ns.query is not None:
+            w(gwa.aligner(fms[0], cfg).align_batch([("read", ns.query, None)]))
+            n = 1
+        else:
+            out.flush()
+            pipe = gwa.Pipeline(fms, cfg, batch_reads=ns.batch, workers_per_device=ns.workers)
+            try:
+                if ns.silent:
+                    with open(os.devnull, "wb") as dn:
+                        n = pipe.align_file(ns.readFiles[0], dn.fileno())
+                else:
+                    try:
+                        fd = out.fileno()
+                    except (AttributeError, io.UnsupportedOperation):
+                        fd = None
+                    if fd is not None:
+                        n = pipe.align_file(ns.readFiles[0], fd)
+                    else:  # an in-memory stream (tests): through a temporary file
+                        with tempfile.TemporaryFile() as tf:
+                            n = pipe.align_file(ns.readFiles[0], tf.fileno())
+                            tf.seek(0)
+                            out.write(tf.read().decode())
+            finally:
+                pipe.close()
+    finally:
+        for fm in fms:
+            fm.close()
     t2 = time.perf_counter()
-    fm.close()
     if ns.timing:
-        print("[gwa] index load %.2fs; align (read file -> SAM, index load excluded) %.2fs: %.0f reads/s"
-              % (t1 - t0, t2 - t1, n / max(t2 - t1, 1e-9)), file=sys.stderr)
+        print("[gwa] index load %.2fs (%d device(s)); align (read file -> SAM, index load excluded) %.2fs: %.0f reads/s"
+              % (t1 - t0, len(devices), t2 - t1, n / max(t2 - t1, 1e-9)), file=sys.stderr)
     return n
+
+
+def bwt(ns):
+    """Build the index of a FASTA on the GPU and save it (the reference's `bwt` command,
+    A/BWTransform.java:72-179, in this build's own format: include/gwa.h gwa_index_save)."""
+    out = ns.out or index_path(ns.fasta)
+    fm = gwa.FMIndexOnGenome.load(ns.fasta, device=ns.device)
+    try:
+        fm.save(out)
+    finally:
+        fm.close()
+    print("[gwa] index of %s saved to %s" % (ns.fasta, out), file=sys.stderr)
 
 
 def main(argv=None):
@@ -184,6 +234,8 @@ def main(argv=None):
         if ns.cmd == "align":
             n = align(ns)
             print("[gwa] %d reads aligned" % n, file=sys.stderr)
+        elif ns.cmd == "bwt":
+            bwt(ns)
     except gwa.GwaError as e:
         print("[gwa] error: %s" % e, file=sys.stderr)
         return 1

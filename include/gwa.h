@@ -81,6 +81,8 @@ typedef struct {
   uint64_t quick_sa_reads; /* of sa_reads, by fm_quickscan */
   uint64_t search_short_steps; /* search FM steps answered by one text character (single-row states) */
   float tier_ms[4];        /* search time per capacity tier (HIP events) */
+  uint64_t num_sw;         /* DP verifications (alignBlockDetailed calls) */
+  uint64_t verify_bytes;   /* SURVEY.md 8(d) bytes of those verifications (reference window + Peq) */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);
@@ -90,8 +92,13 @@ int gwa_device_count(void);
 /* Build an index from FASTA text (the `bwt` command: PackFasta + cyclic SA + BWT) and place
  * it in HBM of `device`. */
 int gwa_index_build_fasta(const char *fasta_text, uint64_t len, int device, gwa_index_t **out);
-/* Same, from a FASTA file path (the `-r` argument). */
+/* Same, from a file (the `-r` argument): a FASTA file, or an index saved by gwa_index_save (recognised
+ * by its magic), which skips the FASTA parse. */
 int gwa_index_open(const char *fasta_path, int device, gwa_index_t **out);
+/* Save an index (2-bit text, N bitmap, contig table; the suffix arrays and Occ blocks are rebuilt on
+ * the GPU at load).  Plays the role of the reference's `bwt` command output (A/BWTransform.java:72-179,
+ * A/BWTFiles.java:40-80) in this build's own format. */
+int gwa_index_save(const gwa_index_t *ix, const char *path);
 /* Same, from codes 0..4 (A,C,G,T,N) and a contig table (names + lengths, concatenated in order). */
 int gwa_index_build_codes(const uint8_t *codes, uint64_t n, int32_t n_contigs, const char *const *names,
                           const int64_t *lengths, int device, gwa_index_t **out);
@@ -122,10 +129,42 @@ int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out);
 /* SAM for reads [first, first+count) only (n_reads = count). */
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out);
 void gwa_batch_free(gwa_batch_t *b);
-/* Instrumentation: per-read counters after gwa_batch_run, 12 int32 per read:
- * status, fm_searches, quick_steps, quickscan_blocks, search_blocks, states, sa_reads, n_hits,
- * quick-scan mismatches/longest-match start (forward, reverse) -- the latter only for searched reads. */
+/* SAM for the reads idx[0..count) in that order (n_reads = count). */
+int gwa_batch_results_select(gwa_batch_t *b, const uint32_t *idx, uint32_t count, gwa_results_t *out);
+/* Instrumentation: per-read counters after gwa_batch_run, GWA_READ_COUNTERS int32 per read:
+ * [0] status, [1] fm_searches (numFMIndexSearches), [2] quick_steps (FMQuickScan steps),
+ * [3] quickscan Occ blocks, [4] search Occ blocks, [5] search states, [6] SA gathers, [7] hits,
+ * [8..11] quick-scan mismatches / longest-match start (forward, reverse; searched reads only),
+ * [12] deepest search tier (-1 = finished in the quick scan), [13] k-mer table lookups,
+ * [14] quick-scan steps answered without Occ blocks, [15] search steps answered from the text,
+ * [16] DP verifications (numSW), [17] SURVEY.md 8(d) verify bytes, [18..19] 0. */
+#define GWA_READ_COUNTERS 20
 int gwa_batch_read_counters(gwa_batch_t *b, int32_t *out);
+
+/* ---- Multi-device driver and overlapped host pipeline (8(f) row 2) ----
+ * Replaces the reference's single-threaded read loop (A/Align.java:174-196: ReadReaderFactory ->
+ * PassReadToAligner -> Aligner.align -> SAMOutput.emit, one read at a time).  A pipeline holds n_ix
+ * index handles -- one per GPU, each a full replica -- and deals read batches of batch_reads reads
+ * to them as they become free (workers_per_device host threads per handle overlap one batch's set-up
+ * and SAM formatting with another's kernels).  Output is in input order, byte-identical to a
+ * single-handle run.  The handles must outlive the pipeline. */
+typedef struct gwa_pipeline gwa_pipeline_t;
+typedef struct {
+  uint64_t reads, batches;
+  double wall_s;               /* the last align / align_file call */
+  double read_s;               /* of which reading (and decompressing) the read file */
+  double device_kernel_s[16];  /* per handle: time inside gwa_batch_run */
+} gwa_pipeline_stats_t;
+int gwa_pipeline_open(gwa_index_t *const *ix, int n_ix, const gwa_config_t *cfg, uint32_t batch_reads,
+                      int workers_per_device, gwa_pipeline_t **out);
+/* SAM (no header) of any number of reads, in input order. */
+int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_t *out);
+/* A FASTA / FASTQ file (.fa .fasta .fan .fastq .fq, optionally .gz; ReadReaderFactory.createReader,
+ * R/ReadReaderFactory.java:126-151) streamed through the devices; SAM records (no header) are
+ * written to fd in input order.  *n_reads = reads aligned. */
+int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_t *n_reads);
+int gwa_pipeline_stats(const gwa_pipeline_t *p, gwa_pipeline_stats_t *st);
+void gwa_pipeline_close(gwa_pipeline_t *p);
 
 #ifdef __cplusplus
 }

@@ -79,6 +79,8 @@ def lib():
         L.orc_fast_count.restype = ctypes.c_int64
         L.orc_fast_count.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
         L.orc_revcomp.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.orc_check_cyclic_sa.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_uint64, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -223,3 +225,15 @@ def revcomp(seq):
     buf = ctypes.create_string_buffer(len(seq) + 16)
     lib().orc_revcomp(seq.encode(), buf, len(seq) + 16)
     return buf.value.decode()
+
+
+def check_cyclic_sa(codes, sa, samples=1 << 20, seed=1, threads=16):
+    """Independent check of a cyclic suffix array of `codes` (permutation + sampled adjacent order);
+    raises AssertionError with the oracle's message on failure (orc_check_cyclic_sa)."""
+    import numpy as np
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    sa = np.ascontiguousarray(sa, dtype=np.uint32)
+    assert len(sa) == len(codes)
+    rc = lib().orc_check_cyclic_sa(codes.ctypes.data, len(codes), sa.ctypes.data, samples, seed, threads)
+    if rc != 0:
+        raise AssertionError("cyclic SA check failed: " + _err())

@@ -35,10 +35,14 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
                            {8192, 8192, 256, 256, 4096, dpw, path, wrn, 1024},
                            {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 16384}};
   std::vector<uint8_t> scratch(std::max(laneBytes<R>(tiers[3]), laneBytes<R>(sfTiers[3])) + ilvBytes(tiers[3]) + 4096);
-  const int chains = cfg.reportType == 0 ? 1 : 4;
-  const int hitCap = chains * (cfg.numSplit + 1), cigCap = 64 * chains;
-  std::vector<OutHit> oh(hitCap);
-  std::vector<uint16_t> oc(cigCap);
+  // one read at a time: a one-slot OutSlots whose pool is large enough for any report
+  const int chains = cfg.reportType == 0 ? 1 : 2;
+  const uint32_t hitCap = chains * (cfg.numSplit + 1), cigCap = 64 * chains;
+  const uint64_t poolH = 1 << 16, poolC = 1 << 20;
+  std::vector<OutHit> oh(hitCap + poolH);
+  std::vector<uint16_t> oc(cigCap + poolC);
+  uint32_t used[3];
+  OutSlots os{oh.data(), oc.data(), hitCap, cigCap, used, hitCap, hitCap + poolH, cigCap, cigCap + poolC};
   std::vector<int32_t> rk = x->h.chrRank;
   for (uint32_t i = 0; i < n; ++i) {
     std::vector<uint8_t> codes;
@@ -57,7 +61,8 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         lane.initRead(codes.data(), (int)mlen);
         hd = OutHeader{};
         lane.sfSearch();
-        lane.writeSearchOutput(&hd, oh.data(), oc.data(), hitCap, cigCap);
+        used[0] = used[1] = used[2] = 0;
+        lane.writeSearchOutput(&hd, os, 0);
         hd.quickSteps = lane.quickSteps;
         if (hd.status != ST_OVERFLOW) break;
         continue;
@@ -70,9 +75,10 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
       if ((tre && atoi(tre) == (int)i) || (qtre && atoi(qtre) == (int)i)) { lane.trace = tv.data() + 1; lane.traceCap = 65536; traced = true; }
       lane.initRead(codes.data(), (int)mlen);
       ScanRes sr{};
-      if (lane.quickPhase(&sr, &hd, oh.data(), oc.data())) {
+      used[0] = used[1] = used[2] = 0;
+      if (lane.quickPhase(&sr, &hd, os, 0)) {
         lane.searchPhase(sr);
-        lane.writeSearchOutput(&hd, oh.data(), oc.data(), hitCap, cigCap);
+        lane.writeSearchOutput(&hd, os, 0);
       }
       if (traced) tv[0] = (uint32_t)lane.traceN;
       if (hd.status != ST_OVERFLOW) break;
@@ -85,8 +91,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
     ReadText rt{names[i], strlen(names[i]), seqs[i], strlen(seqs[i]), quals ? quals[i] : nullptr, (quals && quals[i]) ? strlen(quals[i]) : 0};
     if (!rt.qual) rt.qualLen = 0;
     if (hd.status == ST_MAPPED) {
-      for (int c = 0; c < hd.nChains; ++c)
-        if (formatChain(x->h, rt, oh.data(), oc.data(), hd.chainHead[c], sam) != 0) return -2;
+      if (formatRead(x->h, rt, hd, oh.data(), oc.data(), sam) != 0) return -2;
     } else if (hd.status == ST_UNMAPPED) {
       formatUnmapped(rt, sam);
     } else {

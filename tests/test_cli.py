@@ -48,7 +48,10 @@ def test_options_and_errors():
     assert cfg.k == 2.0 and cfg.reportType == "topL" and cfg.topL == 3 and cfg.bandWidth == 31
     ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "-m", "sf", "r.fq"])
     assert gwa_cli.config_of(ns).strategy == "sf"
-    ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "-m", "bwa", "r.fq"])
+    for m in ("bd", "bwa"):  # BidirectionalBWT: accepted, header-only output (A/Align.java:124-132)
+        ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "-m", m, "r.fq"])
+        assert gwa_cli.config_of(ns).strategy == m
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "-m", "xyz", "r.fq"])
     with pytest.raises(gwa.GwaError):
         gwa_cli.config_of(ns)
     ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa"])
@@ -135,3 +138,61 @@ def test_cli_end_to_end_matches_oracle(tmp_path, fmt):
     oi = O.Index.from_fasta(ref.read_text())
     exp = oi.sam_header() + oi.align(reads, O.OrcConfig.default(k=2.0))
     assert out.getvalue() == exp
+
+
+def _e2e_inputs(tmp_path, fmt, n=700, cid=10):
+    import synth
+    codes, names, lengths = synth.genome([("chrA", 60000), ("chr2", 41000)], config_id=9)
+    ref = tmp_path / "ref.fa"
+    ref.write_text(synth.fasta_text(codes, names, lengths))
+    seqs, rn = synth.reads(codes, lengths, n, 100, 2, config_id=cid)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], "I" * 100 if fmt.startswith("fq") else None) for i in range(len(strs))]
+    rp = tmp_path / ("reads." + fmt)
+    opener = gzip.open if fmt.endswith(".gz") else open
+    with opener(rp, "wt") as f:
+        for nm, sq, q in reads:
+            f.write("@%s\n%s\n+\n%s\n" % (nm, sq, q) if q else ">%s\n%s\n" % (nm, sq))
+    return ref, rp, reads
+
+
+@pytest.mark.gpu
+def test_cli_two_device_handles_match_oracle(tmp_path):
+    # the multi-device pipeline with two index replicas (both on GPU 0 here), small batches dealt
+    # to both, SAM merged in input order == the oracle's
+    import oracle as O
+    ref, rp, reads = _e2e_inputs(tmp_path, "fq", n=3000, cid=11)
+    out = io.StringIO()
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-k", "2", "--batch", "97", "--devices", "0,0",
+                                            str(rp)])
+    assert gwa_cli.align(ns, out=out) == len(reads)
+    oi = O.Index.from_fasta(ref.read_text())
+    assert out.getvalue() == oi.sam_header() + oi.align(reads, O.OrcConfig.default(k=2.0))
+
+
+@pytest.mark.gpu
+def test_saved_index_and_bwt_command(tmp_path):
+    import oracle as O
+    ref, rp, reads = _e2e_inputs(tmp_path, "fq", n=500, cid=12)
+    assert gwa_cli.main(["bwt", str(ref)]) == 0
+    assert os.path.exists(str(ref) + ".gwa.idx")
+    out = io.StringIO()
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-k", "2", str(rp)])
+    assert gwa_cli.align(ns, out=out) == len(reads)
+    oi = O.Index.from_fasta(ref.read_text())
+    assert out.getvalue() == oi.sam_header() + oi.align(reads, O.OrcConfig.default(k=2.0))
+    # the saved file itself loads as an index
+    fm = gwa.FMIndexOnGenome.load(str(ref) + ".gwa.idx")
+    assert fm.samHeader() == oi.sam_header()
+    fm.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", ["bd", "bwa"])
+def test_bd_bwa_print_the_header_only(tmp_path, m):
+    import oracle as O
+    ref, rp, reads = _e2e_inputs(tmp_path, "fq", n=50, cid=13)
+    out = io.StringIO()
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-m", m, str(rp)])
+    assert gwa_cli.align(ns, out=out) == len(reads)
+    assert out.getvalue() == O.Index.from_fasta(ref.read_text()).sam_header()

@@ -239,3 +239,75 @@ def test_text_ends_and_word_boundaries_on_gpu(gwa, strategy):
             reads.append(("e%d_%d" % (i, m), synth.SYM[s].tobytes().decode(), "I" * m))
     for k in (2.0, 0.1):
         _check(gi, oi, reads, k=k, strategy=strategy)
+
+
+# ---- more reported chains than a read's fixed output slot (OutSlots pool) ----
+
+@pytest.fixture(scope="module")
+def many_hits_pair():
+    import genomes
+    codes, names, lengths, reads = genomes.many_hits()
+    gi, oi = _both(codes, names, lengths)
+    return gi, oi, reads
+
+
+@pytest.mark.parametrize("strategy", ["bsf", "sf"])
+@pytest.mark.parametrize("rt", ["allhits", "topl"])
+def test_many_equal_hits_on_gpu(many_hits_pair, strategy, rt):
+    import genomes
+    gi, oi, reads = many_hits_pair
+    sam = _check(gi, oi, reads, k=5.0, reportType=rt, strategy=strategy)
+    assert genomes.max_lines_per_read(sam) >= 5
+
+
+def test_output_pool_growth(many_hits_pair, monkeypatch):
+    # a 4-hit initial pool: the reads that overflow it are rerun after the pool grows
+    gi, oi, reads = many_hits_pair
+    monkeypatch.setenv("GWA_OUT_POOL", "4")
+    _check(gi, oi, reads, k=5.0, reportType="allhits")
+
+
+def test_three_piece_chimeras_two_splits_on_gpu(random_pair):
+    import genomes
+    codes, names, lengths, gi, oi = random_pair
+    for m in (90, 120):
+        _check(gi, oi, genomes.three_fragment_reads(codes, 200, m=m), k=5.0, numSplitAlowed=2)
+
+
+def test_pipeline_two_handles_in_memory(random_pair):
+    # gwa_pipeline_align over two index replicas on GPU 0: batches dealt to both, merged in order
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    gi2 = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths)
+    seqs, rn = synth.reads(codes, lengths, 5000, 100, 2, config_id=31)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
+    pipe = gwa.Pipeline([gi, gi2], gwa.AlignmentConfig(k=2.0), batch_reads=333)
+    got = pipe.align_batch(reads)
+    st = pipe.stats()
+    pipe.close()
+    gi2.close()
+    assert got == oi.align(reads, O.OrcConfig.default(k=2.0))
+    assert st.batches == (5000 + 332) // 333 and st.reads == 5000
+    assert st.device_kernel_s[0] > 0 and st.device_kernel_s[1] > 0
+
+
+def test_per_read_counters_match_oracle_stats(random_pair):
+    # numFMIndexSearches, FMQuickScan steps and DP verifications per read, device vs the oracle's
+    # instrumented restatement (the oracle defines the algorithmic counts)
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 2000, 100, 2, config_id=32)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
+    b = gwa.Batch(gi, gwa.AlignmentConfig(k=2.0), reads)
+    b.run()
+    c = b.read_counters()
+    b.close()
+    _, st = oi.align(reads, O.OrcConfig.default(k=2.0), with_stats=True)
+    fm = np.array([x.fm_searches for x in st])
+    qs = np.array([x.quick_steps for x in st])
+    sw = np.array([x.sw for x in st])
+    assert np.array_equal(c[:, 1], fm), np.nonzero(c[:, 1] != fm)[0][:5]
+    assert np.array_equal(c[:, 2], qs), np.nonzero(c[:, 2] != qs)[0][:5]
+    assert np.array_equal(c[:, 16], sw), np.nonzero(c[:, 16] != sw)[0][:5]

@@ -194,3 +194,28 @@ def test_text_ends_and_word_boundaries(strategy):
             reads.append(("e%d_%d" % (i, m), synth.SYM[s].tobytes().decode(), None))
     for k in (2.0, 0.1):
         _cmp(codes, names, lengths, reads, k, strategy=strategy)
+
+
+# ---- more reported chains than a fixed output slot holds (OutSlots pool), 3-fragment chains ----
+
+@pytest.mark.parametrize("strategy", [0, 1])
+@pytest.mark.parametrize("rt", [1, 2])
+def test_many_equal_hits(strategy, rt):
+    import genomes
+    codes, names, lengths, reads = genomes.many_hits()
+    oi = O.Index.from_arrays(codes, names, lengths)
+    exp = oi.align(reads, O.OrcConfig.default(k=5.0, report_type=rt, strategy=strategy))
+    # some read reports more than 4 chains (allhits) / exactly -L 5 (topL)
+    assert genomes.max_lines_per_read(exp) >= 5
+    _cmp(codes, names, lengths, reads, 5.0, rt=rt, strategy=strategy)
+
+
+def test_three_piece_chimeras_two_splits():
+    # three-piece chimeras at -s 2: the reference keeps at most one split on these (XP has two
+    # states); sam.cpp converts the head and its first split of any longer chain, as
+    # R/AlignmentRecord.java:201-206 does, instead of failing the batch
+    import genomes
+    codes, names, lengths = synth.genome([("c1", 200000), ("c2", 100000)], 5)
+    for m in (90, 120):
+        reads = genomes.three_fragment_reads(codes, 200, m=m)
+        _cmp(codes, names, lengths, reads, 5.0, num_split=2)

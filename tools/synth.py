@@ -1,7 +1,9 @@
 """Synthetic genome / read generator shared by tests and bench.py.
 
-Genome: i.i.d. uniform ACGT contigs (labelled synthetic).  Reads: name r%09d, start uniform
-over the contig, strand 50/50 (- = reverse complement), QUAL 'I'*m, per-config edits.
+Genomes: `genome` = i.i.d. uniform ACGT contigs; `genome_repeats` = hg19-like composition (N gaps,
+interspersed repeat families with divergence, tandem repeats and satellites, segmental
+duplications) at hg19 contig lengths (both labelled synthetic).  Reads: name r%09d, start uniform
+over N-free windows, strand 50/50 (- = reverse complement), QUAL 'I'*m, per-config edits.
 Seeds: 0x6A09E667 ^ config_id (+ shard).  numpy PCG64 streams (not xoshiro).
 """
 import numpy as np
@@ -32,6 +34,133 @@ def genome(contigs, config_id=1, scale=1.0):
     return codes, names, lengths
 
 
+# hg19 gaps that are not sequence: acrocentric short arms and the big chrY heterochromatin block
+_ACRO = {"chr13": 19.0e6, "chr14": 19.0e6, "chr15": 20.0e6, "chr21": 9.4e6, "chr22": 16.0e6}
+
+
+def _mutate(rng, block, div):
+    """Substitute each base of block (uint8 [c, L]) with probability div[c] (per row)."""
+    hit = rng.random(block.shape, dtype=np.float32) < div[:, None]
+    block[hit] = (block[hit] + rng.integers(1, 4, int(hit.sum()), dtype=np.uint8)) % 4
+    return block
+
+
+def _scatter(rng, codes, starts, block):
+    """codes[starts[i] : starts[i] + L] = block[i], keeping N positions (gaps) N."""
+    L = block.shape[1]
+    idx = starts[:, None] + np.arange(L, dtype=np.int64)[None, :]
+    old = codes[idx]
+    codes[idx] = np.where(old == 4, np.uint8(4), block)
+
+
+def genome_repeats(contigs, config_id=1, scale=1.0, log=None):
+    """hg19-like synthetic genome at the given contig lengths -> (codes, names, lengths).
+
+    Composition (approximate hg19 fractions, SURVEY.md §8d "hg19-like N-gap runs", plus the repeat
+    load that makes multi-hit suffix intervals common):
+      N gaps ~6 %: 10 kb telomeres, a 3 Mb centromere per chromosome, acrocentric short arms,
+        chrY heterochromatin, ~8 scattered 50-100 kb gaps per chromosome;
+      Alu-like family (300 bp, ~10 % of sequence, 2-20 % divergence per copy);
+      L1-like family (6 kb consensus, 5'-truncated copies of mean ~1 kb, ~17 %, 3-20 % divergence);
+      24 further interspersed families (150-3000 bp, ~12 %, 5-30 % divergence);
+      alpha-satellite-like 171 bp arrays around centromeres (~2 %, 2-10 % monomer divergence);
+      microsatellites (period 1-6, 20-400 bp, ~1.5 %);
+      segmental duplications (10-200 kb copies of other places, ~4 %, 0.5-5 % divergence).
+    Deterministic for (contigs, config_id, scale)."""
+    rng = np.random.Generator(np.random.PCG64(SEED0 ^ (config_id + 0x5EED)))
+    codes, names, lengths = genome(contigs, config_id, scale)
+    N = len(codes)
+    offs = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+
+    def say(msg):
+        if log:
+            log(msg)
+
+    def spots(count, L):
+        """count random start positions of L-base copies (within one contig each)."""
+        ci = rng.choice(len(lengths), size=count, p=np.array(lengths, np.float64) / N)
+        span = np.maximum(np.array(lengths, np.int64)[ci] - L, 1)
+        return offs[ci] + (rng.random(count) * span).astype(np.int64)
+
+    def family(cons_len, n_copies, dmin, dmax, trunc_mean=None, chunk=100000):
+        cons = rng.integers(0, 4, cons_len, dtype=np.uint8)
+        done = 0
+        while done < n_copies:
+            c = min(chunk, n_copies - done)
+            if trunc_mean is None:
+                L = cons_len
+                blk = np.broadcast_to(cons, (c, L)).copy()
+                _scatter(rng, codes, spots(c, L), _mutate(rng, blk, rng.uniform(dmin, dmax, c).astype(np.float32)))
+            else:  # 5'-truncated copies: a few length classes per chunk
+                for L in np.unique(np.minimum(cons_len, (rng.exponential(trunc_mean, 8) + 200).astype(np.int64))):
+                    cc = max(1, c // 8)
+                    blk = np.broadcast_to(cons[cons_len - L:], (cc, L)).copy()
+                    _scatter(rng, codes, spots(cc, L), _mutate(rng, blk, rng.uniform(dmin, dmax, cc).astype(np.float32)))
+            done += c
+        return cons_len
+
+    # interspersed families (copy counts scale with the genome)
+    g = N / 3.1e9
+    family(300, int(1.0e6 * g), 0.02, 0.20)
+    say("alu-like done")
+    family(6000, int(5.0e5 * g), 0.03, 0.20, trunc_mean=900)
+    say("l1-like done")
+    for f in range(24):
+        L = int(rng.integers(150, 3000))
+        family(L, max(1, int(0.12 * N / 24 / L)), 0.05, 0.30)
+    say("other families done")
+    # microsatellites
+    n_ms = int(0.015 * N / 150)
+    for _ in range(8):
+        per = int(rng.integers(1, 7))
+        unit = rng.integers(0, 4, per, dtype=np.uint8)
+        L = 150
+        blk = np.tile(unit, (n_ms // 8, L // per + 1))[:, :L].copy()
+        _scatter(rng, codes, spots(n_ms // 8, L), _mutate(rng, blk, np.full(n_ms // 8, 0.02, np.float32)))
+    say("microsatellites done")
+    # segmental duplications: copies of other places
+    sd_total, sd = int(0.04 * N), 0
+    while sd < sd_total:
+        L = int(min(rng.integers(10000, 200000), N // 4))
+        src = spots(1, L)[0]
+        dst = spots(1, L)[0]
+        blk = codes[src:src + L][None, :].copy()
+        blk[blk == 4] = 0
+        _scatter(rng, codes, np.array([dst]), _mutate(rng, blk, np.array([rng.uniform(0.005, 0.05)], np.float32)))
+        sd += L
+    say("segmental duplications done")
+    # N gaps and centromeric satellites, per chromosome
+    alpha = rng.integers(0, 4, 171, dtype=np.uint8)
+    for i, (nm, L) in enumerate(zip(names, lengths)):
+        o = offs[i]
+        tel = min(10000, L // 20)
+        codes[o:o + tel] = 4
+        codes[o + L - tel:o + L] = 4
+        if L < 5e6 * scale and L < 2e7:
+            continue
+        if nm in _ACRO:
+            codes[o:o + int(_ACRO[nm] * scale)] = 4
+        if nm == "chrY":
+            a = o + int(0.45 * L)
+            codes[a:a + int(0.5 * L)] = 4
+        cen = o + int(L * rng.uniform(0.3, 0.55))
+        cl = int(3.0e6 * scale)
+        codes[cen:cen + cl] = 4
+        for side in (cen - int(4e5 * scale), cen + cl):  # satellite arrays flanking the centromere gap
+            reps = max(1, int(4e5 * scale) // 171)
+            blk = np.broadcast_to(alpha, (reps, 171)).copy()
+            _mutate(rng, blk, rng.uniform(0.02, 0.10, reps).astype(np.float32))
+            seg = blk.reshape(-1)
+            a = max(o, min(side, o + L - len(seg)))
+            codes[a:a + len(seg)] = np.where(codes[a:a + len(seg)] == 4, np.uint8(4), seg)
+        for _ in range(int(rng.poisson(8))):
+            gl = int(rng.integers(50000, 100000) * scale)
+            a = o + int(rng.random() * max(1, L - gl))
+            codes[a:a + gl] = 4
+    say("gaps done")
+    return codes, names, lengths
+
+
 def reads(codes, lengths, n, m=100, max_subs=2, config_id=2, shard=0, indels=False, max_edits=5):
     """-> (seqs uint8 [n, m] codes, names list) ; substitutions: #subs uniform {0..max_subs},
     distinct positions, base uniform over the other 3."""
@@ -53,6 +182,14 @@ def reads_codes(codes, lengths, n, m=100, max_subs=2, config_id=2, shard=0, inde
         c = min(chunk, n - c0)
         ci = rng.choice(len(L), size=c, p=p)
         starts = offs[ci] + (rng.random(c) * (L[ci] - m - 1)).astype(np.int64)
+        # start uniform over N-free windows: redraw the windows that hold an N
+        for _ in range(64):
+            win = codes[np.minimum(starts[:, None] + np.arange(m + (8 if indels else 0))[None, :], N - 1)]
+            bad = np.nonzero((win == 4).any(axis=1))[0]
+            if len(bad) == 0:
+                break
+            cj = rng.choice(len(L), size=len(bad), p=p)
+            starts[bad] = offs[cj] + (rng.random(len(bad)) * (L[cj] - m - 1)).astype(np.int64)
         if not indels:
             idx = starts[:, None] + np.arange(m)[None, :]
             blk = codes[np.minimum(idx, N - 1)]
