@@ -1,0 +1,192 @@
+// batch_io.hip -- a batch's reads in and SAM text out, on the GPU.
+//
+// Reads in: the caller's read text (names, bases, qualities) is copied to HBM as it is and encoded
+// there -- ACGTSequence(String) (A/ACGTSequence.java:86-97: spaces skipped, ACGT.to3bitCode,
+// A/ACGT.java:36-43) into 16-B aligned, zero-padded code rows (ReadsView).
+//
+// SAM out: the text of a batch is written on the GPU (the reporting tail of the align path:
+// AlignmentRecord.convert / toSAMLine and SAMOutput.emit, R/AlignmentRecord.java:109-276,
+// A/SAMOutput.java:73-82; the per-read logic is sam_core.h).
+//
+// The reference formats one record at a time on the host thread that aligned it.  Here one lane
+// formats one read: a length pass (the writer in counting mode), an exclusive scan of the lengths
+// (rocPRIM), and a write pass that puts every read's records at its offset.  The host receives
+// the finished text of the batch in one copy, in input order.  A read on which the reference
+// would throw (or whose search failed) is reported through `err` (lowest failing position).
+//
+// Also here: the batch statistics as a device reduction over the per-read output headers.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_scan.hpp>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels.h"
+#include "sam_core.h"
+
+namespace gwa {
+
+#define FCHK(x)                                                                                         \
+  do {                                                                                                  \
+    hipError_t e_ = (x);                                                                                \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("sam_format: ") + #x + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---- reads in ----
+
+__device__ __forceinline__ uint8_t to3bitDev(unsigned char c) {
+  switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': case 'U': case 'u': return 3;
+    default: return 4;
+  }
+}
+
+// per read: bases after skipping spaces, its padded row size, and a mark in the length table
+__global__ void __launch_bounds__(256) encodeLenKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqOff,
+                                                       uint32_t n, uint32_t *__restrict__ codeLen,
+                                                       uint32_t *__restrict__ rowLen, uint32_t *__restrict__ lenSeen) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > n) return;
+  if (r == n) {  // the scan's tail: 16 zero bytes after the last row
+    rowLen[n] = 16;
+    return;
+  }
+  uint32_t m = 0;
+  for (uint64_t i = seqOff[r]; i < seqOff[r + 1]; ++i) m += seq[i] != ' ';
+  codeLen[r] = m;
+  rowLen[r] = (m + 15) & ~15u;
+  lenSeen[m < kLenSeen - 1 ? m : kLenSeen - 1] = 1;
+}
+
+__global__ void __launch_bounds__(256) encodeWriteKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqOff,
+                                                         uint32_t n, const uint32_t *__restrict__ codeOff,
+                                                         uint8_t *__restrict__ codes) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  uint8_t *o = codes + codeOff[r];
+  uint32_t k = 0;
+  for (uint64_t i = seqOff[r]; i < seqOff[r + 1]; ++i)
+    if (seq[i] != ' ') o[k++] = to3bitDev((unsigned char)seq[i]);
+  for (const uint32_t e = codeOff[r + 1] - codeOff[r]; k < e; ++k) o[k] = 0;
+}
+
+void launchEncode(const char *seq, const uint64_t *seqOff, uint32_t n, uint32_t *codeLen, uint32_t *rowLen,
+                  uint32_t *codeOff, uint32_t *lenSeen, uint8_t *codes, void *scanTmp, size_t scanTmpBytes, int pass,
+                  hipStream_t s) {
+  const dim3 grid((n + 1 + 255) / 256);
+  if (pass == 0) {
+    hipLaunchKernelGGL(encodeLenKernel, grid, dim3(256), 0, s, seq, seqOff, n, codeLen, rowLen, lenSeen);
+    FCHK(hipGetLastError());
+    size_t b = scanTmpBytes;
+    FCHK(rocprim::exclusive_scan(scanTmp, b, rowLen, codeOff, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), s));
+  } else {
+    hipLaunchKernelGGL(encodeWriteKernel, grid, dim3(256), 0, s, seq, seqOff, n, codeOff, codes);
+    FCHK(hipGetLastError());
+  }
+}
+
+size_t encodeScanTempBytes(uint32_t n) {
+  size_t b = 0;
+  FCHK(rocprim::exclusive_scan(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t)0, (size_t)n + 1,
+                               rocprim::plus<uint32_t>(), (hipStream_t)0));
+  return b;
+}
+
+// ---- SAM out ----
+
+__global__ void __launch_bounds__(256) samLenKernel(SamText t, const OutHeader *__restrict__ oh, const OutHit *__restrict__ hits,
+                                                    const uint16_t *__restrict__ cig, const uint32_t *__restrict__ idx,
+                                                    uint32_t first, uint32_t n, uint64_t *__restrict__ len,
+                                                    uint32_t *__restrict__ err) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > n) return;
+  if (j == n) {  // the scan's total
+    len[n] = 0;
+    return;
+  }
+  const uint32_t r = idx ? idx[j] : first + j;
+  SamOut o{nullptr, 0};
+  if (samRead(o, t, r, oh[r], hits, cig) != 0) {
+    atomicMin(err, j);
+    o.n = 0;
+  }
+  len[j] = o.n;
+}
+
+__global__ void __launch_bounds__(256) samWriteKernel(SamText t, const OutHeader *__restrict__ oh, const OutHit *__restrict__ hits,
+                                                      const uint16_t *__restrict__ cig, const uint32_t *__restrict__ idx,
+                                                      uint32_t first, uint32_t n, const uint64_t *__restrict__ off,
+                                                      char *__restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t r = idx ? idx[j] : first + j;
+  SamOut o{out + off[j], 0};
+  (void)samRead(o, t, r, oh[r], hits, cig);
+}
+
+void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
+                     uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
+                     uint32_t *err, char *out, int pass, hipStream_t s) {
+  const dim3 grid((n + 1 + 255) / 256);
+  if (pass == 0) {
+    hipLaunchKernelGGL(samLenKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, len, err);
+    FCHK(hipGetLastError());
+  } else if (pass == 1) {  // exclusive scan of n + 1 lengths: off[n] = total bytes
+    FCHK(rocprim::exclusive_scan(scanTmp, *scanTmpBytes, len, off, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), s));
+  } else {
+    hipLaunchKernelGGL(samWriteKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, off, out);
+    FCHK(hipGetLastError());
+  }
+}
+
+size_t samScanTempBytes(uint32_t n) {
+  size_t b = 0;
+  FCHK(rocprim::exclusive_scan(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, (size_t)n + 1,
+                               rocprim::plus<uint64_t>(), (hipStream_t)0));
+  return b;
+}
+
+// Batch statistics: sums of the per-read instrumentation (gwa_batch_stats_t), one atomic per
+// workgroup and field.
+__global__ void __launch_bounds__(256) statsKernel(const OutHeader *__restrict__ oh, uint32_t n,
+                                                   unsigned long long *__restrict__ acc) {
+  __shared__ unsigned long long sh[kStatFields];
+  if (threadIdx.x < kStatFields) sh[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long v[kStatFields];
+  for (int f = 0; f < kStatFields; ++f) v[f] = 0;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    const OutHeader &h = oh[r];
+    v[0] += (unsigned)h.fmSearches;
+    v[1] += (unsigned)h.quickSteps;
+    v[2] += (unsigned)h.blocks;
+    v[3] += (unsigned)h.searchBlocks;
+    v[4] += (unsigned)h.kmerLookups;
+    v[5] += (unsigned)h.saReads;
+    v[6] += (unsigned)h.quickSa;
+    v[7] += (unsigned)h.quickShort;
+    v[8] += (unsigned)h.searchShort;
+    v[9] += (unsigned)h.states;
+    v[10] += (unsigned)h.numSW;
+    v[11] += (unsigned)h.verifyBytes;
+    v[12] += h.status == ST_MAPPED;
+    v[13] += h.status == ST_UNMAPPED;
+  }
+  for (int f = 0; f < kStatFields; ++f) atomicAdd(&sh[f], v[f]);
+  __syncthreads();
+  if (threadIdx.x < kStatFields) atomicAdd(&acc[threadIdx.x], sh[threadIdx.x]);
+}
+
+void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipStream_t s) {
+  FCHK(hipMemsetAsync(acc, 0, kStatFields * sizeof(unsigned long long), s));
+  if (n == 0) return;
+  const uint32_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(statsKernel, dim3(g > 2048 ? 2048 : g), dim3(256), 0, s, oh, n, acc);
+  FCHK(hipGetLastError());
+}
+
+}  // namespace gwa

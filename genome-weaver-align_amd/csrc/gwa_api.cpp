@@ -20,6 +20,7 @@
 #include "host_index.h"
 #include "kernels.h"
 #include "sam.h"
+#include "sam_core.h"
 
 using namespace gwa;
 
@@ -70,7 +71,10 @@ struct gwa_index {
   uint64_t *d_text2 = nullptr, *d_textN = nullptr;
   uint64_t *d_kmer[2] = {nullptr, nullptr};
   int64_t *d_contig = nullptr;
-  int32_t *d_chrRank = nullptr;
+  int32_t *d_chrRank = nullptr;  // String.compareTo rank of each contig name (also its SAM name key)
+  char *d_ctg = nullptr;         // contig names (SAM RNAME / RNEXT text)
+  uint64_t *d_ctgOff = nullptr;
+  int32_t starKey = -3, emptyKey = -2;  // name keys of "*" and "" (SamText)
   size_t bytes = 0;
   IndexView view{};
   // reusable search scratch: one batch at a time runs its kernels on the index (runMu); batch set-up
@@ -86,14 +90,21 @@ struct gwa_batch {
   hipStream_t stream = nullptr;
   gwa_config_t cfg{};
   SearchConfig scfg{};
-  // host copy of the reads (SAM needs names, sequences, qualities)
   uint32_t n = 0;
-  std::string names, seqs, quals;
-  std::vector<uint64_t> nameOff, seqOff, qualOff;
   bool hasQual = false;
-  std::vector<uint8_t> codes;
-  std::vector<uint32_t> codeOff, codeLen;
   int maxM = 0, kmax = 0, R = 4;
+  // the read text in HBM (offsets rebased to 0): bases (encoded on the device into d_codes), names
+  // and qualities (read by the SAM writer)
+  char *d_seq = nullptr, *d_name = nullptr, *d_qual = nullptr;
+  uint64_t *d_seqOff = nullptr, *d_nameOff = nullptr, *d_qualOff = nullptr;
+  // SAM formatting buffers (grown on demand) and the statistics accumulator
+  uint64_t *d_fmtLen = nullptr, *d_fmtOff = nullptr;
+  uint32_t *d_fmtIdx = nullptr, *d_fmtErr = nullptr;
+  void *d_fmtTmp = nullptr;
+  char *d_fmtText = nullptr;
+  size_t fmtCap = 0, fmtTmpBytes = 0, fmtTextCap = 0;
+  unsigned long long *d_stats = nullptr;
+  bool statsDone = false;
   // device
   uint8_t *d_codes = nullptr;
   uint32_t *d_off = nullptr, *d_len = nullptr;
@@ -110,12 +121,8 @@ struct gwa_batch {
   uint64_t poolHits = 0, poolCig = 0;  // OutSlots pool behind the fixed slots (grown on demand)
   uint64_t poolUsedH = 0, poolUsedC = 0;
   StairTables st{};
-  // results
-  std::vector<OutHeader> oh;
-  std::vector<OutHit> hits;
-  std::vector<uint16_t> cig;
   gwa_batch_stats_t stats{};
-  bool ran = false, fetched = false;
+  bool ran = false;
   bool headerOnly = false;  // -m bd / -m bwa: the reference emits no SAM records (see gwa_batch_create)
   std::vector<std::pair<uint32_t, int>> deep;  // (read, tier) of every read rerun on a tier >= 1
 };
@@ -131,6 +138,8 @@ static void freeIndexDev(gwa_index *ix) {
   if (ix->d_textN) (void)hipFree(ix->d_textN);
   if (ix->d_contig) (void)hipFree(ix->d_contig);
   if (ix->d_chrRank) (void)hipFree(ix->d_chrRank);
+  if (ix->d_ctg) (void)hipFree(ix->d_ctg);
+  if (ix->d_ctgOff) (void)hipFree(ix->d_ctgOff);
   if (ix->scratch) (void)hipFree(ix->scratch);
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
 }
@@ -191,6 +200,15 @@ static void buildFromDeviceText(gwa_index *ix, uint8_t *dT) {
   rankNames(h);
   ix->d_contig = devUpload(h.offsets, s, &ix->bytes);
   ix->d_chrRank = devUpload(h.chrRank, s, &ix->bytes);
+  {  // contig names for the SAM writer
+    const SamNames sn = samNames(h);
+    std::vector<char> blob(sn.blob.begin(), sn.blob.end());
+    blob.push_back(0);
+    ix->d_ctg = devUpload(blob, s, &ix->bytes);
+    ix->d_ctgOff = devUpload(sn.off, s, &ix->bytes);
+    ix->starKey = sn.starKey;
+    ix->emptyKey = sn.emptyKey;
+  }
   HIPCHK(hipStreamSynchronize(s));
   IndexView &v = ix->view;
   v.occ[0] = ix->d_occ[0]; v.occ[1] = ix->d_occ[1];
@@ -453,7 +471,8 @@ void gwa_free(void *p) { free(p); }
 
 static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
-                b->d_stair, b->d_stairBase};
+                b->d_stair, b->d_stairBase, b->d_seq, b->d_name, b->d_qual, b->d_seqOff, b->d_nameOff, b->d_qualOff,
+                b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats};
   for (void *p : ps)
     if (p) (void)hipFree(p);
   if (b->stream) (void)hipStreamDestroy(b->stream);
@@ -487,62 +506,56 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     const uint32_t n = reads->n;
     b->n = n;
     b->hasQual = reads->qual != nullptr;
-    b->nameOff.assign(reads->name_off, reads->name_off + n + 1);
-    b->seqOff.assign(reads->seq_off, reads->seq_off + n + 1);
-    b->names.assign(reads->name + b->nameOff[0], reads->name + b->nameOff[n]);
-    b->seqs.assign(reads->seq + b->seqOff[0], reads->seq + b->seqOff[n]);
-    if (b->hasQual) {
-      b->qualOff.assign(reads->qual_off, reads->qual_off + n + 1);
-      b->quals.assign(reads->qual + b->qualOff[0], reads->qual + b->qualOff[n]);
-    }
-    // codes (ACGTSequence(String): spaces skipped, A/ACGTSequence.java:86-97), each read 16-B
-    // aligned and zero-padded (ReadsView); encoded on up to 16 host threads in two passes (lengths,
-    // then codes at the prefix-summed offsets)
-    b->codeOff.resize(n + 1);
-    b->codeLen.resize(n);
-    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    auto parallel = [&](auto fn) {
-      std::vector<std::thread> th;
-      for (unsigned t = 0; t < nt; ++t)
-        th.emplace_back([&, t] { fn((uint32_t)((uint64_t)n * t / nt), (uint32_t)((uint64_t)n * (t + 1) / nt)); });
-      for (auto &x : th) x.join();
+    HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    hipStream_t s = b->stream;
+    // the read text goes to HBM as it is (offsets rebased to the blob starts) and is encoded there
+    // (batch_io.hip: ACGTSequence(String), A/ACGTSequence.java:86-97)
+    auto blob = [&](const char *base, const uint64_t *off, char **dText, uint64_t **dOff) {
+      std::vector<uint64_t> o(off, off + n + 1);
+      const uint64_t o0 = o[0];
+      for (auto &x : o) x -= o0;
+      *dText = devAlloc<char>(o[n] + 1);
+      if (o[n]) HIPCHK(hipMemcpyAsync(*dText, base + o0, o[n], hipMemcpyHostToDevice, s));
+      *dOff = devUpload(o, s, nullptr);
+      HIPCHK(hipStreamSynchronize(s));  // (o is a local vector)
+      return o[n];
     };
-    const char *sq = b->seqs.data();
-    const uint64_t s0 = b->seqOff[0];
-    parallel([&](uint32_t a, uint32_t e) {
-      for (uint32_t i = a; i < e; ++i) {
-        const char *p = sq + (b->seqOff[i] - s0);
-        const uint64_t L = b->seqOff[i + 1] - b->seqOff[i];
-        uint32_t m = 0;
-        for (uint64_t j = 0; j < L; ++j) m += p[j] != ' ';
-        b->codeLen[i] = m;
-      }
-    });
-    uint64_t tot = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-      if (tot > 0xFFFFFFFFull) throw std::runtime_error("read batch too large (> 4 GiB of codes)");
-      b->codeOff[i] = (uint32_t)tot;
-      tot += ((uint64_t)b->codeLen[i] + 15) & ~(uint64_t)15;
+    const uint64_t seqBytes = blob(reads->seq, reads->seq_off, &b->d_seq, &b->d_seqOff);
+    blob(reads->name, reads->name_off, &b->d_name, &b->d_nameOff);
+    if (b->hasQual) blob(reads->qual, reads->qual_off, &b->d_qual, &b->d_qualOff);
+    const uint64_t codeBound = seqBytes + 16ull * n + 32;
+    if (codeBound > 0xFFFFFFFFull) throw std::runtime_error("read batch too large (> 4 GiB of codes): use fewer reads per batch");
+    b->d_codes = devAlloc<uint8_t>(codeBound);
+    b->d_off = devAlloc<uint32_t>((size_t)n + 1);
+    b->d_len = devAlloc<uint32_t>((size_t)n + 1);
+    uint32_t *d_row = devAlloc<uint32_t>((size_t)n + 1);
+    uint32_t *d_seen = devAlloc<uint32_t>(kLenSeen);
+    const size_t tmpBytes = encodeScanTempBytes(n);
+    void *d_tmp = devAlloc<uint8_t>(tmpBytes);
+    std::vector<uint32_t> seen(kLenSeen);
+    try {
+      HIPCHK(hipMemsetAsync(d_seen, 0, kLenSeen * sizeof(uint32_t), s));
+      launchEncode(b->d_seq, b->d_seqOff, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 0, s);
+      launchEncode(b->d_seq, b->d_seqOff, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 1, s);
+      HIPCHK(hipMemcpyAsync(seen.data(), d_seen, kLenSeen * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    } catch (...) {
+      (void)hipFree(d_row);
+      (void)hipFree(d_seen);
+      (void)hipFree(d_tmp);
+      throw;
     }
-    b->codes.assign(tot + 16, 0);
-    b->codeOff[n] = (uint32_t)(tot + 16);
-    parallel([&](uint32_t a, uint32_t e) {
-      for (uint32_t i = a; i < e; ++i) {
-        const char *p = sq + (b->seqOff[i] - s0);
-        const uint64_t L = b->seqOff[i + 1] - b->seqOff[i];
-        uint8_t *o = b->codes.data() + b->codeOff[i];
-        for (uint64_t j = 0; j < L; ++j)
-          if (p[j] != ' ') *o++ = to3bit((unsigned char)p[j]);
-      }
-    });
+    (void)hipFree(d_row);
+    (void)hipFree(d_seen);
+    (void)hipFree(d_tmp);
+    // the distinct read lengths: maximum length, k per length (AlignmentScoreConfig
+    // .getMaximumEditDistance) and the staircase tables
     std::vector<int> lens;
-    std::vector<char> seen(256, 0);
-    for (uint32_t i = 0; i < n; ++i) {
-      const int m = (int)b->codeLen[i];
-      b->maxM = std::max(b->maxM, m);
-      if (m <= 255 && !seen[(size_t)m]) { seen[(size_t)m] = 1; lens.push_back(m); }
-    }
-    // k per length (AlignmentScoreConfig.getMaximumEditDistance)
+    for (uint32_t m = 0; m < kLenSeen; ++m)
+      if (seen[m]) {
+        b->maxM = (int)m;
+        if (m <= 255) lens.push_back((int)m);
+      }
     for (int m : lens) {
       int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
       b->kmax = std::max(b->kmax, k);
@@ -552,11 +565,6 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     std::vector<uint64_t> tab;
     std::vector<uint32_t> base;
     buildStairTables(lens, std::max(b->kmax, 0), tab, base);
-    HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-    hipStream_t s = b->stream;
-    b->d_codes = devUpload(b->codes, s, nullptr);
-    b->d_off = devUpload(b->codeOff, s, nullptr);
-    b->d_len = devUpload(b->codeLen, s, nullptr);
     b->d_stair = devUpload(tab, s, nullptr);
     b->d_stairBase = devUpload(base, s, nullptr);
     b->st.tab = b->d_stair;
@@ -687,7 +695,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       b->ran = true;
       return 0;
     }
-    b->ran = b->fetched = false;
+    b->ran = b->statsDone = false;
     b->poolUsedH = b->poolUsedC = 0;
     b->deep.clear();
     ReadsView rv{b->d_codes, b->d_off, b->d_len, b->n};
@@ -811,134 +819,161 @@ int gwa_batch_run(gwa_batch_t *b) {
   }
 }
 
-int gwa_batch_stats(const gwa_batch_t *b, gwa_batch_stats_t *st) {
-  *st = b->stats;
-  return 0;
-}
-
-static int fetch(gwa_batch *b) {
-  if (b->fetched || b->headerOnly) return 0;
-  const uint32_t n = b->n;
-  b->oh.resize(n);
-  b->hits.resize((size_t)n * b->hitCap + b->poolUsedH);
-  b->cig.resize((size_t)n * b->cigCap + b->poolUsedC);
-  HIPCHK(hipSetDevice(b->ix->device));
-  hipStream_t s = b->stream;
-  HIPCHK(hipMemcpyAsync(b->oh.data(), b->d_oh, n * sizeof(OutHeader), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(b->hits.data(), b->d_hits, b->hits.size() * sizeof(OutHit), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(b->cig.data(), b->d_cig, b->cig.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  gwa_batch_stats_t &st = b->stats;
-  st.fm_searches = st.quick_steps = st.blocks = st.states = st.quick_blocks = st.sa_reads = st.kmer_lookups = 0;
-  st.quick_short_steps = st.quick_sa_reads = st.search_short_steps = 0;
-  st.n_mapped = st.n_unmapped = 0;
-  st.num_sw = st.verify_bytes = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const OutHeader &h = b->oh[i];
-    st.fm_searches += (uint64_t)h.fmSearches;
-    st.quick_steps += (uint64_t)h.quickSteps;
-    st.blocks += (uint64_t)h.blocks + (uint64_t)h.searchBlocks;
-    st.quick_blocks += (uint64_t)h.blocks;
-    st.kmer_lookups += (uint64_t)h.kmerLookups;
-    st.sa_reads += (uint64_t)h.saReads + (uint64_t)h.quickSa;
-    st.quick_sa_reads += (uint64_t)h.quickSa;
-    st.quick_short_steps += (uint64_t)h.quickShort;
-    st.search_short_steps += (uint64_t)h.searchShort;
-    st.states += (uint64_t)h.states;
-    st.num_sw += (uint64_t)h.numSW;
-    st.verify_bytes += (uint64_t)h.verifyBytes;
-    if (h.status == ST_MAPPED) st.n_mapped++;
-    else if (h.status == ST_UNMAPPED) st.n_unmapped++;
-  }
-  b->fetched = true;
-  return 0;
-}
-
 }  // extern "C"
 
-// SAM text of the reads idx(0), ..., idx(count - 1), formatted on up to 16 host threads
-template <class Idx>
-static void formatSelected(gwa_batch *b, Idx idx, uint32_t count, gwa_results_t *out) {
+// the batch statistics (gwa_batch_stats_t sums) as one device reduction over the output headers
+static void ensureStats(gwa_batch *b) {
+  if (b->statsDone || b->headerOnly || !b->ran) return;
+  HIPCHK(hipSetDevice(b->ix->device));
+  hipStream_t s = b->stream;
+  if (!b->d_stats) b->d_stats = devAlloc<unsigned long long>(kStatFields);
+  launchStats(b->d_oh, b->n, b->d_stats, s);
+  unsigned long long v[kStatFields];
+  HIPCHK(hipMemcpyAsync(v, b->d_stats, sizeof(v), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  gwa_batch_stats_t &st = b->stats;
+  st.fm_searches = v[0];
+  st.quick_steps = v[1];
+  st.quick_blocks = v[2];
+  st.blocks = v[2] + v[3];
+  st.kmer_lookups = v[4];
+  st.quick_sa_reads = v[6];
+  st.sa_reads = v[5] + v[6];
+  st.quick_short_steps = v[7];
+  st.search_short_steps = v[8];
+  st.states = v[9];
+  st.num_sw = v[10];
+  st.verify_bytes = v[11];
+  st.n_mapped = (uint32_t)v[12];
+  st.n_unmapped = (uint32_t)v[13];
+  b->statsDone = true;
+}
+
+static SamText samText(const gwa_batch *b) {
+  SamText t;
+  t.name = b->d_name;
+  t.nameOff = b->d_nameOff;
+  t.qual = b->hasQual ? b->d_qual : nullptr;
+  t.qualOff = b->d_qualOff;
+  t.codes = b->d_codes;
+  t.codeOff = b->d_off;
+  t.codeLen = b->d_len;
+  t.ctg = b->ix->d_ctg;
+  t.ctgOff = b->ix->d_ctgOff;
+  t.chrKey = b->ix->d_chrRank;
+  t.starKey = b->ix->starKey;
+  t.emptyKey = b->ix->emptyKey;
+  return t;
+}
+
+template <class T>
+static void growDev(T **p, size_t *cap, size_t need) {
+  if (*p && *cap >= need) return;
+  if (*p) HIPCHK(hipFree(*p));
+  *p = nullptr;
+  *p = devAlloc<T>(need);
+  *cap = need;
+}
+
+// SAM text of the reads idx[0..count) (or first .. first + count - 1) written on the device
+// (batch_io.hip), copied to library-owned host memory in one piece
+static void formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t first, uint32_t count, gwa_results_t *out) {
   if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
-  fetch(b);
   const uint32_t n = count;
+  out->n_reads = n;
+  out->sam = nullptr;
+  out->line_off = nullptr;
   if (b->headerOnly) {
-    out->n_reads = n;
     out->sam = (char *)calloc(1, 1);
     out->sam_len = 0;
     out->line_off = (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t));
     return;
   }
-  for (uint32_t j = 0; j < n; ++j) {
-    const uint32_t i = idx(j);
-    int stt = b->oh[i].status;
-    if (stt == ST_ERROR || stt == ST_OVERFLOW || stt == ST_TOO_LONG) {
-      std::string nm(b->names.data() + (b->nameOff[i] - b->nameOff[0]), b->nameOff[i + 1] - b->nameOff[i]);
-      throw std::runtime_error(std::string(stt == ST_ERROR ? "reference would abort (exception) at read "
-                                                           : stt == ST_TOO_LONG ? "read longer than the device path supports: "
-                                                                                : "output slot overflow at read ") + nm);
-    }
+  HIPCHK(hipSetDevice(b->ix->device));
+  hipStream_t s = b->stream;
+  if (!b->d_fmtLen || b->fmtCap < (size_t)n + 1) {
+    void *ps[] = {b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtTmp};
+    for (void *p : ps)
+      if (p) (void)hipFree(p);
+    b->d_fmtLen = b->d_fmtOff = nullptr;
+    b->d_fmtIdx = nullptr;
+    b->d_fmtTmp = nullptr;
+    b->d_fmtLen = devAlloc<uint64_t>((size_t)n + 1);
+    b->d_fmtOff = devAlloc<uint64_t>((size_t)n + 1);
+    b->d_fmtIdx = devAlloc<uint32_t>((size_t)n + 1);
+    b->fmtTmpBytes = samScanTempBytes(n);
+    b->d_fmtTmp = devAlloc<uint8_t>(b->fmtTmpBytes);
+    b->fmtCap = (size_t)n + 1;
   }
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  std::vector<std::string> parts(nt);
-  std::vector<std::vector<uint64_t>> lens(nt);
-  std::atomic<int> bad{-1};
-  auto work = [&](unsigned t) {
-    uint32_t a = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
-    std::string &o = parts[t];
-    o.reserve((size_t)(e - a) * 320);
-    for (uint32_t j = a; j < e; ++j) {
-      const uint32_t i = idx(j);
-      size_t before = o.size();
-      ReadText rt;
-      rt.name = b->names.data() + (b->nameOff[i] - b->nameOff[0]);
-      rt.nameLen = b->nameOff[i + 1] - b->nameOff[i];
-      rt.seq = b->seqs.data() + (b->seqOff[i] - b->seqOff[0]);
-      rt.seqLen = b->seqOff[i + 1] - b->seqOff[i];
-      if (b->hasQual) {
-        rt.qual = b->quals.data() + (b->qualOff[i] - b->qualOff[0]);
-        rt.qualLen = b->qualOff[i + 1] - b->qualOff[i];
-      } else {
-        rt.qual = nullptr;
-        rt.qualLen = 0;
-      }
-      const OutHeader &h = b->oh[i];
-      if (h.status == ST_MAPPED) {
-        if (formatRead(b->ix->host, rt, h, b->hits.data(), b->cig.data(), o) != 0) bad = (int)i;
-      } else {
-        formatUnmapped(rt, o);
-      }
-      lens[t].push_back(o.size() - before);
-    }
-  };
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, t);
-  for (auto &x : th) x.join();
-  if (bad >= 0) throw std::runtime_error("reference would abort (exception in AlignmentRecord.convert) at read index " + std::to_string(bad.load()));
-  size_t total = 0;
-  for (auto &p : parts) total += p.size();
-  out->n_reads = n;
+  if (!b->d_fmtErr) b->d_fmtErr = devAlloc<uint32_t>(1);
+  const uint32_t *dIdx = nullptr;
+  if (hostIdx) {
+    HIPCHK(hipMemcpyAsync(b->d_fmtIdx, hostIdx, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    dIdx = b->d_fmtIdx;
+  }
+  HIPCHK(hipMemsetAsync(b->d_fmtErr, 0xFF, sizeof(uint32_t), s));
+  const SamText t = samText(b);
+  size_t tmpBytes = b->fmtTmpBytes;
+  launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
+                  b->d_fmtErr, nullptr, 0, s);
+  launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
+                  b->d_fmtErr, nullptr, 1, s);
+  uint64_t total = 0;
+  uint32_t err = 0;
+  HIPCHK(hipMemcpyAsync(&total, b->d_fmtOff + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&err, b->d_fmtErr, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (err != 0xFFFFFFFFu) {  // a read the reference would abort on, or whose search failed
+    const uint32_t r = hostIdx ? hostIdx[err] : first + err;
+    OutHeader h;
+    uint64_t no[2];
+    HIPCHK(hipMemcpy(&h, b->d_oh + r, sizeof(h), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(no, b->d_nameOff + r, sizeof(no), hipMemcpyDeviceToHost));
+    std::string nm(no[1] - no[0], '\0');
+    if (!nm.empty()) HIPCHK(hipMemcpy(&nm[0], b->d_name + no[0], nm.size(), hipMemcpyDeviceToHost));
+    const int stt = h.status;
+    throw std::runtime_error(std::string(stt == ST_TOO_LONG ? "read longer than the device path supports: "
+                                         : stt == ST_OVERFLOW ? "output slot overflow at read "
+                                         : stt == ST_ERROR ? "reference would abort (exception) at read "
+                                                           : "reference would abort (exception in AlignmentRecord.convert) at read ") + nm);
+  }
+  growDev(&b->d_fmtText, &b->fmtTextCap, (size_t)total + 1);
+  launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
+                  b->d_fmtErr, b->d_fmtText, 2, s);
   out->sam = (char *)malloc(total + 1);
-  out->sam_len = total;
-  out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
-  size_t pos = 0;
-  uint32_t ri = 0;
-  for (unsigned t = 0; t < nt; ++t) {
-    memcpy(out->sam + pos, parts[t].data(), parts[t].size());
-    for (uint64_t L : lens[t]) { out->line_off[ri++] = pos; pos += L; }
+  out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n + 1));
+  if (!out->sam || !out->line_off) {
+    free(out->sam);
+    free(out->line_off);
+    out->sam = nullptr;
+    out->line_off = nullptr;
+    throw std::runtime_error("out of host memory for the SAM text");
   }
-  out->line_off[n] = pos;
+  if (total) HIPCHK(hipMemcpyAsync(out->sam, b->d_fmtText, total, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(out->line_off, b->d_fmtOff, sizeof(uint64_t) * ((size_t)n + 1), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   out->sam[total] = 0;
+  out->sam_len = total;
 }
 
 extern "C" {
+
+int gwa_batch_stats(gwa_batch_t *b, gwa_batch_stats_t *st) {
+  try {
+    ensureStats(b);
+    *st = b->stats;
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
 
 int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) { return gwa_batch_results_range(b, 0, b->n, out); }
 
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out) {
   try {
     if ((uint64_t)first + count > b->n) throw std::runtime_error("result range out of bounds");
-    formatSelected(b, [first](uint32_t j) { return first + j; }, count, out);
+    formatOnDevice(b, nullptr, first, count, out);
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());
@@ -949,7 +984,7 @@ int gwa_batch_results_select(gwa_batch_t *b, const uint32_t *idx, uint32_t count
   try {
     for (uint32_t j = 0; j < count; ++j)
       if (idx[j] >= b->n) throw std::runtime_error("result index out of bounds");
-    formatSelected(b, [idx](uint32_t j) { return idx[j]; }, count, out);
+    formatOnDevice(b, idx, 0, count, out);
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());
@@ -960,11 +995,13 @@ int gwa_batch_read_counters(gwa_batch_t *b, int32_t *out) {
   try {
     if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
     if (b->headerOnly) throw std::runtime_error("-m bd / -m bwa batches have no device counters");
-    fetch(b);
+    HIPCHK(hipSetDevice(b->ix->device));
+    std::vector<OutHeader> oh(b->n);
     std::vector<ScanRes> sr(b->n);
+    HIPCHK(hipMemcpy(oh.data(), b->d_oh, b->n * sizeof(OutHeader), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(sr.data(), b->d_sres, b->n * sizeof(ScanRes), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < b->n; ++i) {
-      const OutHeader &h = b->oh[i];
+      const OutHeader &h = oh[i];
       int32_t *o = out + (size_t)i * GWA_READ_COUNTERS;
       o[8] = sr[i].nmF; o[9] = sr[i].lmF; o[10] = sr[i].nmR; o[11] = sr[i].lmR;
       o[0] = h.status; o[1] = h.fmSearches; o[2] = h.quickSteps; o[3] = h.blocks; o[4] = h.searchBlocks;

@@ -23,6 +23,20 @@ void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const Se
                     const Caps &caps, OutHeader *oh, const OutSlots &os,
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s);
 void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream_t s);
+
+// batch_io.hip: reads in (encode on the device), SAM out (two-pass formatting), batch statistics
+struct SamText;
+constexpr uint32_t kLenSeen = 65536;  // read-length presence table (lengths >= 65535 share the last slot)
+constexpr int kStatFields = 14;
+void launchEncode(const char *seq, const uint64_t *seqOff, uint32_t n, uint32_t *codeLen, uint32_t *rowLen,
+                  uint32_t *codeOff, uint32_t *lenSeen, uint8_t *codes, void *scanTmp, size_t scanTmpBytes, int pass,
+                  hipStream_t s);
+size_t encodeScanTempBytes(uint32_t n);
+void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
+                     uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
+                     uint32_t *err, char *out, int pass, hipStream_t s);
+size_t samScanTempBytes(uint32_t n);
+void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipStream_t s);
 size_t laneBytesFor(int R, const Caps &c);  // per-lane slice
 size_t ilvBytesFor(const Caps &c);          // per-lane share of the interleaved DP block
 

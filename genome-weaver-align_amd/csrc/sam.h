@@ -1,26 +1,21 @@
 // sam.h -- host-side AlignmentRecord conversion + SAM text
 #pragma once
 #include <string>
+#include <vector>
 
 #include "host_index.h"
 
 namespace gwa {
 
-struct ReadText {
-  const char *name;
-  size_t nameLen;
-  const char *seq;
-  size_t seqLen;
-  const char *qual;  // nullptr == no quality (Java null -> "*")
-  size_t qualLen;
-};
-
 std::string samHeader(const HostIndex &ix);
-int formatChain(const HostIndex &ix, const ReadText &rt, const OutHit *hits, const uint16_t *cig, int head, std::string &out);
-void formatUnmapped(const ReadText &rt, std::string &out);
-// every reported chain of a mapped read (OutHeader: hits and CIGAR ops at hitOff / cigOff, chains
-// back to back); 0, or -1 where the reference would throw
-int formatRead(const HostIndex &ix, const ReadText &rt, const OutHeader &h, const OutHit *hits, const uint16_t *cig,
-               std::string &out);
+
+// Contig names as the SAM writer (sam_core.h SamText) reads them: one blob + offsets, and the keys
+// of the names "*" and "" (the contig's chrRank when a contig carries that name)
+struct SamNames {
+  std::string blob;
+  std::vector<uint64_t> off;
+  int32_t starKey, emptyKey;
+};
+SamNames samNames(const HostIndex &ix);
 
 }  // namespace gwa

@@ -1,0 +1,353 @@
+// sam_core.h -- the SAM records of one read, written by one GPU lane (or by the host test harness):
+//   AlignmentRecord.convert   (R/AlignmentRecord.java:181-276)
+//   AlignmentRecord.toSAMLine (R/AlignmentRecord.java:109-170)
+//   SAMOutput.emit            (A/SAMOutput.java:73-82)
+// The same function measures a record (SamOut with p == nullptr counts bytes) and writes it, so the
+// device formats a batch in two passes: lengths, an exclusive scan, then every read's text at its
+// offset (sam_format.hip).  SAM flag values follow the SAM spec (utgb SAMReadFlag is unvendored;
+// SURVEY.md §8c).
+#pragma once
+#include "gwa_layout.h"
+
+namespace gwa {
+
+// Read text and contig names as the formatter reads them (device or host memory).  Offsets are
+// relative to the blob starts.
+struct SamText {
+  const char *name;
+  const uint64_t *nameOff;   // n + 1
+  const char *qual;          // nullptr: no qualities (SAM "*", as for FASTA input)
+  const uint64_t *qualOff;   // n + 1
+  const uint8_t *codes;      // ReadsView: the read as codes 0..4 (spaces skipped)
+  const uint32_t *codeOff, *codeLen;
+  const char *ctg;           // contig names
+  const uint64_t *ctgOff;    // nContig + 1
+  const int32_t *chrKey;     // per contig: equal names <=> equal keys (String.equals)
+  int32_t starKey, emptyKey; // the keys of the names "*" and "" (a contig may be called that)
+};
+
+// byte sink: counts when p == nullptr
+struct SamOut {
+  char *p;
+  uint64_t n;
+  GWA_HD void ch(char c) {
+    if (p) p[n] = c;
+    ++n;
+  }
+  GWA_HD void bytes(const char *s, uint64_t len) {
+    if (p)
+      for (uint64_t i = 0; i < len; ++i) p[n + i] = s[i];
+    n += len;
+  }
+  template <unsigned long L>
+  GWA_HD void lit(const char (&s)[L]) {  // a string literal (without its terminating 0)
+    bytes(s, L - 1);
+  }
+  GWA_HD void num(int64_t v) {  // Integer.toString
+    char b[24];
+    int k = 0;
+    const bool neg = v < 0;
+    uint64_t u = neg ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    do {
+      b[k++] = (char)('0' + (int)(u % 10));
+      u /= 10;
+    } while (u);
+    if (neg) ch('-');
+    while (k) ch(b[--k]);
+  }
+};
+
+namespace samfmt {
+
+constexpr char kSym[5] = {'A', 'C', 'G', 'T', 'N'};
+constexpr char kOp[8] = {'M', 'I', 'D', 'N', 'S', 'H', 'P', 'X'};
+
+GWA_HD char stateCh(int numHits) { return numHits > 0 ? (numHits == 1 ? 'U' : 'R') : 'N'; }
+
+// CIGAR of a record as items: elements copied from a hit's list keep that list as it is (a fresh
+// CIGAR built from an element list), later add() calls merge with the last element
+// (CIGAR.add, A/CIGAR.java:158-170)
+struct CigSpec {
+  const uint16_t *a;  // first element list (raw), or nullptr
+  int na;
+  int preS;           // -1, or add(S, preS) first (on an empty CIGAR)
+  int postS;          // -1, or add(S, postS) after list a
+  const uint16_t *b;  // elements added one by one after list a (merged), or nullptr
+  int nb;
+};
+
+struct CigEmit {
+  SamOut &o;
+  int pt = -1;
+  int64_t pl = 0;
+  GWA_HD explicit CigEmit(SamOut &o_) : o(o_) {}
+  GWA_HD void flush() {
+    if (pt >= 0) {
+      o.num(pl);
+      o.ch(kOp[pt & 7]);
+    }
+  }
+  GWA_HD void raw(int t, int64_t l) {
+    flush();
+    pt = t;
+    pl = l;
+  }
+  GWA_HD void add(int t, int64_t l) {
+    if (pt == t) pl += l;
+    else raw(t, l);
+  }
+};
+
+GWA_HD void emitCigar(SamOut &o, const CigSpec &c) {
+  CigEmit e(o);
+  if (c.preS >= 0) e.add(4, c.preS);
+  for (int i = 0; i < c.na; ++i) e.raw(c.a[i] & 7, c.a[i] >> 3);
+  if (c.postS >= 0) e.add(4, c.postS);
+  for (int i = 0; i < c.nb; ++i) e.add(c.b[i] & 7, c.b[i] >> 3);
+  e.flush();
+}
+
+// one AlignmentRecord to print
+struct Rec {
+  int chr, strand, start, end, nm, numBestHits;
+  CigSpec cig;
+  int seqA, seqB;       // SEQ = the strand-oriented query [seqA, seqB)
+  int qualA, qualB;     // QUAL = the strand-oriented quality [qualA, qualB)
+  int stateHead, stateSelf;  // XP = ReadHit.getAlignmentState over the chain from stateHead
+  bool hasSplit;
+};
+
+struct Ctx {
+  const SamText &t;
+  uint32_t r;
+  const OutHit *hits;   // the read's hits (chain indices are relative to this)
+  int m;
+  int strand;           // of the chain head: orientation of SEQ / QUAL
+  bool qualNull;
+  uint64_t q0, qn;      // quality text [q0, q0 + qn)
+  bool npe = false;     // the reference would throw
+};
+
+GWA_HD int32_t nameKey(const Ctx &cx, int chr) {
+  if (chr >= 0) return cx.t.chrKey[chr];
+  if (chr == CHR_STAR) return cx.t.starKey;
+  if (chr == CHR_EMPTY) return cx.t.emptyKey;
+  return -2147483647 - 1;
+}
+
+GWA_HD void chrName(SamOut &o, Ctx &cx, int chr) {
+  if (chr >= 0) o.bytes(cx.t.ctg + cx.t.ctgOff[chr], cx.t.ctgOff[chr + 1] - cx.t.ctgOff[chr]);
+  else if (chr == CHR_STAR) o.ch('*');
+  else if (chr == CHR_EMPTY) {
+  } else cx.npe = true;  // null chr
+}
+
+GWA_HD void emitSeq(SamOut &o, const Ctx &cx, int a, int b) {
+  const uint8_t *c = cx.t.codes + cx.t.codeOff[cx.r];
+  for (int j = a; j < b; ++j) {
+    const uint8_t x = cx.strand == 0 ? c[j] : c[cx.m - 1 - j];
+    o.ch(kSym[cx.strand == 0 ? x : (x < 4 ? 3 - x : 4)]);
+  }
+}
+
+GWA_HD void emitQual(SamOut &o, const Ctx &cx, int a, int b) {
+  if (cx.qualNull) {
+    o.ch('*');
+    return;
+  }
+  const char *q = cx.t.qual + cx.q0;
+  for (int j = a; j < b; ++j) o.ch(cx.strand == 0 ? q[j] : q[cx.qn - 1 - j]);
+}
+
+GWA_HD void emitState(SamOut &o, const Ctx &cx, int head, int self) {
+  for (int t = head; t >= 0; t = cx.hits[t].next) {
+    const char c = stateCh(cx.hits[t].numHits);
+    o.ch(t == self ? c : (char)(c - 'A' + 'a'));
+  }
+}
+
+// AlignmentRecord.toSAMLine (R/AlignmentRecord.java:109-170) of one record; returns the
+// eachFragmentIsMapped value handed on to the split record's line
+GWA_HD bool lineOne(SamOut &o, Ctx &cx, const Rec &r, const Rec *split, bool hasSegments, bool isFirst, bool eachMapped) {
+  int flag = 0;
+  if (hasSegments) flag |= 0x1;
+  if (r.strand == 1) flag |= 0x10;
+  if (isFirst) {
+    flag |= 0x40;
+    if (r.numBestHits <= 0 || (split && split->numBestHits <= 0)) eachMapped = false;
+  } else if (!split) {
+    flag |= 0x80;
+  }
+  if (eachMapped) flag |= 0x2;
+  if (r.numBestHits <= 0) flag |= 0x4;
+  if (split && split->numBestHits <= 0) flag |= 0x8;
+  o.bytes(cx.t.name + cx.t.nameOff[cx.r], cx.t.nameOff[cx.r + 1] - cx.t.nameOff[cx.r]);
+  o.ch('\t');
+  o.num(flag);
+  o.ch('\t');
+  chrName(o, cx, r.chr);
+  o.ch('\t');
+  o.num(r.start);
+  o.lit("\t1\t");  // MAPQ column = AlignmentRecord.score, always 1 (:199)
+  emitCigar(o, r.cig);
+  if (!split) {
+    o.lit("\t*\t0\t0");
+  } else {
+    const int32_t ck = nameKey(cx, r.chr), sk = nameKey(cx, split->chr);
+    if (r.chr != CHR_NULL && split->chr != CHR_NULL && ck != cx.t.starKey && ck == sk) {
+      o.lit("\t=");
+    } else {
+      o.ch('\t');
+      chrName(o, cx, split->chr);
+    }
+    o.ch('\t');
+    o.num(split->start);
+    o.ch('\t');
+    o.num((int64_t)split->end - r.start);
+  }
+  o.ch('\t');
+  emitSeq(o, cx, r.seqA, r.seqB);
+  o.ch('\t');
+  emitQual(o, cx, r.qualA, r.qualB);
+  if (r.numBestHits > 0) {
+    if (r.nm >= 0) {
+      o.lit("\tNM:i:");
+      o.num(r.nm);
+    }
+    o.lit("\tXP:Z:");
+    emitState(o, cx, r.stateHead, r.stateSelf);
+    o.lit("\tX0:i:");
+    o.num(r.numBestHits);
+  }
+  return eachMapped;
+}
+
+// a record and, when it has one, its split record on the next line
+GWA_HD void emitRec(SamOut &o, Ctx &cx, const Rec &r, const Rec *split, bool hasSegments) {
+  const bool em = lineOne(o, cx, r, split, hasSegments, true, true);
+  if (split) {
+    o.ch('\n');
+    lineOne(o, cx, *split, nullptr, hasSegments, false, em);
+  }
+}
+
+}  // namespace samfmt
+
+// One reported ReadHit chain (head = index into hits) -> SAM text, '\n' terminated.  Returns 0, or
+// -1 where the reference would throw (the run aborts, S/BidirectionalSuffixFilter.java:264-267).
+GWA_HD int samChain(SamOut &o, const SamText &t, uint32_t r, const OutHit *hits, const uint16_t *cig, int head) {
+  using namespace samfmt;
+  const OutHit &h = hits[head];
+  Ctx cx{t, r, hits, (int)t.codeLen[r], h.strand != 0 ? 1 : 0, t.qual == nullptr, 0, 0};
+  if (!cx.qualNull) {
+    cx.q0 = t.qualOff[r];
+    cx.qn = t.qualOff[r + 1] - t.qualOff[r];
+  }
+  const int m = cx.m;
+  const int fullQual = cx.qualNull ? 0 : (int)cx.qn;
+  Rec rec{};
+  rec.cig = CigSpec{cig + h.cigarOff, (int)h.cigarLen, -1, -1, nullptr, 0};
+  rec.seqA = 0; rec.seqB = m;
+  rec.qualA = 0; rec.qualB = fullQual;
+  rec.stateHead = head;
+  rec.stateSelf = head;
+  if (h.next < 0) {
+    rec.chr = h.chr; rec.strand = h.strand; rec.start = h.pos; rec.end = h.pos + h.matchLength; rec.nm = h.diff;
+    rec.numBestHits = h.numHits;
+    emitRec(o, cx, rec, nullptr, false);
+  } else {
+    // the head and its first split are converted; later fragments of a longer chain are dropped
+    // (R/AlignmentRecord.java:201-206 reads hit.nextSplit only), but still named in XP
+    const OutHit &s = hits[h.next];
+    const int numHits = h.numHits;
+    const int qualLen = !cx.qualNull ? (int)cx.qn : h.matchLength;
+    const bool hU = h.numHits == 1, sU = s.numHits == 1;
+    // substrings taken by convert (:187-196): a bad range is a Java exception
+    auto bad = [](int a, int b, int size) { return a < 0 || b > size || a > b; };
+    const int b1 = qualLen < h.matchLength ? qualLen : h.matchLength;
+    const int b2 = qualLen < m ? qualLen : m;
+    if (bad(h.qStart, h.qEnd, m) || bad(s.qStart, s.qEnd, m)) return -1;
+    if (!cx.qualNull && (bad(0, b1, (int)cx.qn) || bad(b1, b2, (int)cx.qn))) return -1;
+    if (hU) {
+      if (sU) {
+        if (h.chr == CHR_NULL) return -1;
+        bool same = (h.chr >= 0 && s.chr >= 0) ? t.chrKey[h.chr] == t.chrKey[s.chr] : h.chr == s.chr;
+        if (s.chr == CHR_NULL) same = false;
+        if (same) {
+          Rec srec{};
+          rec.chr = h.chr; rec.strand = h.strand; rec.start = h.pos; rec.end = h.pos + h.matchLength; rec.nm = h.diff;
+          rec.seqA = h.qStart; rec.seqB = h.qEnd; rec.qualA = 0; rec.qualB = b1; rec.numBestHits = 1;
+          srec.chr = s.chr; srec.strand = s.strand; srec.start = s.pos; srec.end = s.pos + s.matchLength; srec.nm = s.diff;
+          srec.cig = CigSpec{cig + s.cigarOff, (int)s.cigarLen, -1, -1, nullptr, 0};
+          srec.seqA = s.qStart; srec.seqB = s.qEnd; srec.qualA = b1; srec.qualB = b2; srec.numBestHits = 1;
+          srec.stateHead = head;
+          srec.stateSelf = h.next;
+          if (cx.qualNull) { rec.qualB = srec.qualB = 0; }
+          emitRec(o, cx, rec, &srec, true);
+        } else if (h.matchLength >= s.matchLength) {
+          rec.cig.postS = s.matchLength;
+          rec.chr = h.chr; rec.strand = h.strand; rec.start = h.pos; rec.end = h.pos + m; rec.nm = h.diff;
+          rec.numBestHits = numHits;
+          emitRec(o, cx, rec, nullptr, false);
+        } else {
+          if (s.chr == CHR_NULL) return -1;
+          rec.cig.b = cig + s.cigarOff;
+          rec.cig.nb = (int)s.cigarLen;
+          rec.chr = s.chr; rec.strand = s.strand; rec.start = s.pos - h.matchLength; rec.end = s.pos - h.matchLength + m;
+          rec.nm = s.diff; rec.numBestHits = numHits; rec.stateSelf = h.next;
+          emitRec(o, cx, rec, nullptr, false);
+        }
+      } else {
+        if (h.chr == CHR_NULL) return -1;
+        rec.cig.postS = s.qEnd - s.qStart;
+        rec.chr = h.chr; rec.strand = h.strand; rec.start = h.pos; rec.end = h.pos; rec.nm = h.diff;
+        rec.numBestHits = numHits;
+        emitRec(o, cx, rec, nullptr, false);
+      }
+    } else {
+      if (!sU) return 0;  // convert returns null: SAMOutput.emit prints nothing (:78-81)
+      if (s.chr == CHR_NULL) return -1;
+      rec.cig = CigSpec{nullptr, 0, h.matchLength, -1, cig + s.cigarOff, (int)s.cigarLen};
+      rec.chr = s.chr; rec.strand = s.strand; rec.start = s.pos - h.matchLength; rec.end = s.pos - h.matchLength + m;
+      rec.nm = s.diff; rec.numBestHits = numHits; rec.stateSelf = h.next;
+      emitRec(o, cx, rec, nullptr, false);
+    }
+  }
+  o.ch('\n');
+  return cx.npe ? -1 : 0;
+}
+
+// The unmapped record: ReadHit("*", 0, 0, 0, 0, -1, FORWARD, CIGAR(), 0)
+// (S/BidirectionalSuffixFilter.java:258-261)
+GWA_HD void samUnmapped(SamOut &o, const SamText &t, uint32_t r) {
+  o.bytes(t.name + t.nameOff[r], t.nameOff[r + 1] - t.nameOff[r]);
+  o.lit("\t68\t*\t0\t1\t\t*\t0\t0\t");
+  const uint8_t *c = t.codes + t.codeOff[r];
+  for (uint32_t j = 0; j < t.codeLen[r]; ++j) o.ch(samfmt::kSym[c[j] > 4 ? 4 : c[j]]);
+  o.ch('\t');
+  if (t.qual) o.bytes(t.qual + t.qualOff[r], t.qualOff[r + 1] - t.qualOff[r]);
+  else o.ch('*');
+  o.ch('\n');
+}
+
+// Every record of read r: its reported chains (OutHeader: hits at hitOff, CIGAR ops at cigOff,
+// chains back to back) or the unmapped record.  0, or -1 where the reference would throw.
+GWA_HD int samRead(SamOut &o, const SamText &t, uint32_t r, const OutHeader &h, const OutHit *hits, const uint16_t *cig) {
+  if (h.status == ST_UNMAPPED) {
+    samUnmapped(o, t, r);
+    return 0;
+  }
+  if (h.status != ST_MAPPED) return -1;
+  const OutHit *hb = hits + h.hitOff;
+  const uint16_t *cb = cig + h.cigOff;
+  int head = 0;
+  for (int c = 0; c < h.nChains; ++c) {
+    if (samChain(o, t, r, hb, cb, head) != 0) return -1;
+    int x = head;
+    while (hb[x].next >= 0) x = hb[x].next;
+    head = x + 1;
+  }
+  return 0;
+}
+
+}  // namespace gwa

@@ -124,7 +124,7 @@ void gwa_reads_free(gwa_read_buf_t *b);
  * then fetch results. */
 int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_batch_t **out);
 int gwa_batch_run(gwa_batch_t *b);
-int gwa_batch_stats(const gwa_batch_t *b, gwa_batch_stats_t *st);
+int gwa_batch_stats(gwa_batch_t *b, gwa_batch_stats_t *st);
 int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out);
 /* SAM for reads [first, first+count) only (n_reads = count). */
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out);

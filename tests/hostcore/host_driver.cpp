@@ -12,6 +12,7 @@
 #include "../../genome-weaver-align_amd/csrc/sf_core.h"
 #include "../../genome-weaver-align_amd/csrc/host_index.h"
 #include "../../genome-weaver-align_amd/csrc/sam.h"
+#include "../../genome-weaver-align_amd/csrc/sam_core.h"
 
 using namespace gwa;
 
@@ -44,6 +45,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
   uint32_t used[3];
   OutSlots os{oh.data(), oc.data(), hitCap, cigCap, used, hitCap, hitCap + poolH, cigCap, cigCap + poolC};
   std::vector<int32_t> rk = x->h.chrRank;
+  const SamNames sn = samNames(x->h);
   for (uint32_t i = 0; i < n; ++i) {
     std::vector<uint8_t> codes;
     for (const char *c = seqs[i]; *c; ++c)
@@ -88,12 +90,19 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
       if (tf) { fwrite(tv.data(), 4, 1 + tv[0], tf); fclose(tf); }
     }
     if (stats) { stats[i * 4] = hd.fmSearches; stats[i * 4 + 1] = hd.quickSteps; stats[i * 4 + 2] = hd.maxHeap; stats[i * 4 + 3] = hd.states; }
-    ReadText rt{names[i], strlen(names[i]), seqs[i], strlen(seqs[i]), quals ? quals[i] : nullptr, (quals && quals[i]) ? strlen(quals[i]) : 0};
-    if (!rt.qual) rt.qualLen = 0;
-    if (hd.status == ST_MAPPED) {
-      if (formatRead(x->h, rt, hd, oh.data(), oc.data(), sam) != 0) return -2;
-    } else if (hd.status == ST_UNMAPPED) {
-      formatUnmapped(rt, sam);
+    // the device SAM writer (sam_core.h) on the host, for this one read
+    const char *qv = quals ? quals[i] : nullptr;
+    const uint64_t nameOff[2] = {0, strlen(names[i])}, qualOff[2] = {0, qv ? strlen(qv) : 0};
+    const uint32_t codeOff[1] = {0}, codeLen[1] = {(uint32_t)mlen};
+    const SamText t{names[i], nameOff, qv, qualOff, codes.data(), codeOff, codeLen, sn.blob.data(), sn.off.data(),
+                    rk.data(), sn.starKey, sn.emptyKey};
+    if (hd.status == ST_MAPPED || hd.status == ST_UNMAPPED) {
+      SamOut cnt{nullptr, 0};
+      if (samRead(cnt, t, 0, hd, oh.data(), oc.data()) != 0) return -2;
+      const size_t at = sam.size();
+      sam.resize(at + cnt.n);
+      SamOut o{&sam[at], 0};
+      samRead(o, t, 0, hd, oh.data(), oc.data());
     } else {
       fprintf(stderr, "hc: status %d at read %u\n", hd.status, i);
       return -1 - hd.status;

@@ -19,6 +19,10 @@ def main():
     ap.add_argument("--genome", default="hg19")
     ap.add_argument("--reads", type=int, default=2_000_000)
     ap.add_argument("--gz", action="store_true")
+    ap.add_argument("--saved-index", action="store_true", help="run the `bwt` command first; align loads its index")
+    ap.add_argument("--devices", default=None)
+    ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 20)
     a = ap.parse_args()
     import gzip
     import numpy as np
@@ -52,13 +56,20 @@ def main():
     print("[e2e] inputs written in %.1fs: %s (%.2f GB), %s (%.2f GB)"
           % (time.time() - t0, fa, os.path.getsize(fa) / 1e9, fq, os.path.getsize(fq) / 1e9), flush=True)
     out = os.path.join(d, "out.sam")
+    cli = [sys.executable, os.path.join(REPO, "genome-weaver-align_amd", "gwa_cli.py")]
+    if a.saved_index:
+        t0 = time.time()
+        r = subprocess.run(cli + ["bwt", fa], stderr=subprocess.PIPE, text=True)
+        print("[e2e] bwt (FASTA -> saved index) %.1fs rc %d %s" % (time.time() - t0, r.returncode, r.stderr.strip()), flush=True)
     t0 = time.time()
-    r = subprocess.run([sys.executable, os.path.join(REPO, "genome-weaver-align_amd", "gwa_cli.py"), "align", "-r", fa,
-                        "-k", "2", "--timing", fq], stdout=open(out, "wb"), stderr=subprocess.PIPE, text=True)
+    extra = (["--devices", a.devices] if a.devices else []) + ["--workers", str(a.workers), "--batch", str(a.batch)]
+    r = subprocess.run(cli + ["align", "-r", fa, "-k", "2", "--timing"] + extra + [fq], stdout=open(out, "wb"),
+                       stderr=subprocess.PIPE, text=True)
     print(r.stderr.strip(), flush=True)
     print("[e2e] CLI wall %.1fs, SAM %.2f GB, rc %d" % (time.time() - t0, os.path.getsize(out) / 1e9, r.returncode))
-    for p in (fa, fq, out):
-        os.remove(p)
+    for p in (fa, fq, out, fa + ".gwa.idx"):
+        if os.path.exists(p):
+            os.remove(p)
     os.rmdir(d)
     sys.exit(r.returncode)
 
