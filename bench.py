@@ -221,6 +221,45 @@ def main():
         log("host pipeline: %.0f reads/s (setup %.2fs, kernels %.2fs, SAM %.2fs, %.2f GB)"
             % (pipe["reads_per_s"], t1 - t0, t2 - t1, t3 - t2, nbytes / 1e9))
 
+    # end to end (first bullet): this batch's reads as a FASTQ file on local disk ->
+    # the library pipeline (gwa_pipeline_align_file: read, frame, H2D, parse + encode + align + SAM on
+    # the GPU, D2H, write) -> a SAM file; index load excluded
+    e2e = None
+    if rank == 0 and not args.no_pipeline and not c4:
+        import tempfile
+        d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+        fq, so = os.path.join(d, "reads.fq"), os.path.join(d, "out.sam")
+        t0 = time.perf_counter()
+        rec = np.empty((reads_per_step, 12 + m + 3 + m + 1), dtype=np.uint8)  # "@r%09d\n" seq "\n+\n" qual "\n"
+        rec[:, 0] = ord("@")
+        rec[:, 1:11] = np.frombuffer(name_blob, dtype=np.uint8).reshape(reads_per_step, 10)
+        rec[:, 11] = ord("\n")
+        rec[:, 12:12 + m] = np.frombuffer(seq_blob, dtype=np.uint8).reshape(reads_per_step, m)
+        rec[:, 12 + m:15 + m] = np.frombuffer(b"\n+\n", dtype=np.uint8)
+        rec[:, 15 + m:15 + 2 * m] = ord("I")
+        rec[:, 15 + 2 * m] = ord("\n")
+        with open(fq, "wb") as f:
+            f.write(rec.data)
+        del rec
+        t_write = time.perf_counter() - t0
+        pipe_ = gwa.Pipeline([gi], cfg)
+        with open(so, "wb") as f:
+            t0 = time.perf_counter()
+            n_e2e = pipe_.align_file(fq, f.fileno())
+            t_e2e = time.perf_counter() - t0
+        pst = pipe_.stats()
+        pipe_.close()
+        e2e = {"reads_per_s": n_e2e / t_e2e, "seconds": t_e2e, "reads": n_e2e, "fastq_bytes": os.path.getsize(fq),
+               "sam_bytes": os.path.getsize(so), "fastq_write_s": t_write,
+               "stages_s": {"read": pst.read_s, "frame": pst.frame_s, "setup": pst.setup_s,
+                            "kernels": pst.device_kernel_s[0], "sam_format_d2h": pst.format_s, "write": pst.write_s},
+               "note": "FASTQ file -> SAM file through gwa_pipeline_align_file (1 GPU, 2 worker threads), local "
+                       "disk via the page cache; index load excluded; stage times summed over threads"}
+        log("end to end FASTQ -> SAM: %.0f reads/s (%d reads in %.2fs)" % (n_e2e / t_e2e, n_e2e, t_e2e))
+        for x in (fq, so):
+            os.remove(x)
+        os.rmdir(d)
+
     counters = batch.read_counters()  # also fetches the records (stats below)
     st = batch.stats()
     total_reads = reads_per_step * args.steps * world
@@ -336,7 +375,7 @@ def main():
                    "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
                    "tier_ms": [round(x, 3) for x in st.tier_ms], "dp_verifications_per_read": st.num_sw / reads_per_step,
                    "quick_short_steps_per_read": st.quick_short_steps / reads_per_step,
-                   "cpu_baseline_1thread": cpu1, "host_pipeline": pipe,
+                   "cpu_baseline_1thread": cpu1, "host_pipeline": pipe, "end_to_end": e2e,
                    "search_short_steps_per_read": st.search_short_steps / reads_per_step,
                    "rank_kernel": {"kernel": "fm_quickscan", "definition": "SURVEY.md 8(d) algorithmic bytes",
                                    "algorithmic_bytes_per_launch": q_ref, "avg_launch_ms": q_ms,

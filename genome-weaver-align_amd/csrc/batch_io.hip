@@ -46,8 +46,8 @@ __device__ __forceinline__ uint8_t to3bitDev(unsigned char c) {
 }
 
 // per read: bases after skipping spaces, its padded row size, and a mark in the length table
-__global__ void __launch_bounds__(256) encodeLenKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqOff,
-                                                       uint32_t n, uint32_t *__restrict__ codeLen,
+__global__ void __launch_bounds__(256) encodeLenKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqB,
+                                                       const uint64_t *__restrict__ seqE, uint32_t n, uint32_t *__restrict__ codeLen,
                                                        uint32_t *__restrict__ rowLen, uint32_t *__restrict__ lenSeen) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r > n) return;
@@ -56,35 +56,36 @@ __global__ void __launch_bounds__(256) encodeLenKernel(const char *__restrict__ 
     return;
   }
   uint32_t m = 0;
-  for (uint64_t i = seqOff[r]; i < seqOff[r + 1]; ++i) m += seq[i] != ' ';
+  for (uint64_t i = seqB[r]; i < seqE[r]; ++i) m += seq[i] != ' ';
   codeLen[r] = m;
   rowLen[r] = (m + 15) & ~15u;
   lenSeen[m < kLenSeen - 1 ? m : kLenSeen - 1] = 1;
 }
 
-__global__ void __launch_bounds__(256) encodeWriteKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqOff,
-                                                         uint32_t n, const uint32_t *__restrict__ codeOff,
+__global__ void __launch_bounds__(256) encodeWriteKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqB,
+                                                         const uint64_t *__restrict__ seqE, uint32_t n,
+                                                         const uint32_t *__restrict__ codeOff,
                                                          uint8_t *__restrict__ codes) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   uint8_t *o = codes + codeOff[r];
   uint32_t k = 0;
-  for (uint64_t i = seqOff[r]; i < seqOff[r + 1]; ++i)
+  for (uint64_t i = seqB[r]; i < seqE[r]; ++i)
     if (seq[i] != ' ') o[k++] = to3bitDev((unsigned char)seq[i]);
   for (const uint32_t e = codeOff[r + 1] - codeOff[r]; k < e; ++k) o[k] = 0;
 }
 
-void launchEncode(const char *seq, const uint64_t *seqOff, uint32_t n, uint32_t *codeLen, uint32_t *rowLen,
+void launchEncode(const char *seq, const uint64_t *seqB, const uint64_t *seqE, uint32_t n, uint32_t *codeLen, uint32_t *rowLen,
                   uint32_t *codeOff, uint32_t *lenSeen, uint8_t *codes, void *scanTmp, size_t scanTmpBytes, int pass,
                   hipStream_t s) {
   const dim3 grid((n + 1 + 255) / 256);
   if (pass == 0) {
-    hipLaunchKernelGGL(encodeLenKernel, grid, dim3(256), 0, s, seq, seqOff, n, codeLen, rowLen, lenSeen);
+    hipLaunchKernelGGL(encodeLenKernel, grid, dim3(256), 0, s, seq, seqB, seqE, n, codeLen, rowLen, lenSeen);
     FCHK(hipGetLastError());
     size_t b = scanTmpBytes;
     FCHK(rocprim::exclusive_scan(scanTmp, b, rowLen, codeOff, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), s));
   } else {
-    hipLaunchKernelGGL(encodeWriteKernel, grid, dim3(256), 0, s, seq, seqOff, n, codeOff, codes);
+    hipLaunchKernelGGL(encodeWriteKernel, grid, dim3(256), 0, s, seq, seqB, seqE, n, codeOff, codes);
     FCHK(hipGetLastError());
   }
 }
@@ -94,6 +95,59 @@ size_t encodeScanTempBytes(uint32_t n) {
   FCHK(rocprim::exclusive_scan(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t)0, (size_t)n + 1,
                                rocprim::plus<uint32_t>(), (hipStream_t)0));
   return b;
+}
+
+// FASTQ records straight from the file text (the pipeline's zero-copy path): record r starts at
+// start[r] (its header line; the host framed the text into complete records, reads_io.cpp
+// frameRecords).  The fields are located under the record rules of reads_io.cpp parseFastq: lines
+// end at "\n", "\r\n" or "\r"; a line missing at the end of the text reads as ""; the name is the
+// first whitespace-delimited token after '@'; the third line must start with '+' and the quality
+// must be as long as the sequence.  A malformed record sets err (lowest record index); the host
+// then re-parses the text to report it as the host parser words it.
+__device__ __forceinline__ bool isWsDev(unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r') || (c >= 0x1c && c <= 0x1f); }
+
+__device__ __forceinline__ uint64_t lineAt(const char *__restrict__ t, uint64_t len, uint64_t pos, uint64_t *e) {
+  if (pos >= len) {
+    *e = len;
+    return len;
+  }
+  uint64_t i = pos;
+  while (i < len && t[i] != '\n' && t[i] != '\r') ++i;
+  *e = i;
+  if (i == len) return len;
+  if (t[i] == '\r' && i + 1 < len && t[i + 1] == '\n') return i + 2;
+  return i + 1;
+}
+
+__global__ void __launch_bounds__(256) fastqFieldsKernel(const char *__restrict__ t, uint64_t len, const uint64_t *__restrict__ start,
+                                                         uint32_t n, uint64_t *__restrict__ f, uint32_t *__restrict__ err) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  uint64_t he, se, pe, qe;
+  const uint64_t hb = start[r];
+  const uint64_t sb = lineAt(t, len, hb, &he);
+  const uint64_t pb = lineAt(t, len, sb, &se);
+  const uint64_t qb = lineAt(t, len, pb, &pe);
+  (void)lineAt(t, len, qb, &qe);
+  if (he == hb || t[hb] != '@' || pe == pb || t[pb] != '+' || qe - qb != se - sb) atomicMin(err, r);
+  uint64_t nb = hb + 1;
+  while (nb < he && isWsDev((unsigned char)t[nb])) ++nb;
+  uint64_t ne = nb;
+  while (ne < he && !isWsDev((unsigned char)t[ne])) ++ne;
+  // six field arrays of n: name [b, e), sequence [b, e), quality [b, e)
+  f[r] = nb;
+  f[(size_t)n + r] = ne;
+  f[2 * (size_t)n + r] = sb;
+  f[3 * (size_t)n + r] = se;
+  f[4 * (size_t)n + r] = qb;
+  f[5 * (size_t)n + r] = qe;
+}
+
+void launchFastqFields(const char *text, uint64_t len, const uint64_t *start, uint32_t n, uint64_t *fields,
+                       uint32_t *err, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(fastqFieldsKernel, dim3((n + 255) / 256), dim3(256), 0, s, text, len, start, n, fields, err);
+  FCHK(hipGetLastError());
 }
 
 // ---- SAM out ----

@@ -93,10 +93,13 @@ struct gwa_batch {
   uint32_t n = 0;
   bool hasQual = false;
   int maxM = 0, kmax = 0, R = 4;
-  // the read text in HBM (offsets rebased to 0): bases (encoded on the device into d_codes), names
-  // and qualities (read by the SAM writer)
-  char *d_seq = nullptr, *d_name = nullptr, *d_qual = nullptr;
-  uint64_t *d_seqOff = nullptr, *d_nameOff = nullptr, *d_qualOff = nullptr;
+  // the read text in HBM: bases (encoded on the device into d_codes), names and qualities (read by
+  // the SAM writer).  Read r's bases are d_seqText[d_seqB[r], d_seqE[r]) etc.: SoA blobs (E = B + 1)
+  // or, from the pipeline, the fields of FASTQ records inside one copy of the file text.
+  char *d_seqText = nullptr, *d_nameText = nullptr, *d_qualText = nullptr;
+  const uint64_t *d_seqB = nullptr, *d_seqE = nullptr, *d_nameB = nullptr, *d_nameE = nullptr;
+  const uint64_t *d_qualB = nullptr, *d_qualE = nullptr;
+  uint64_t *d_fieldOwn[3] = {nullptr, nullptr, nullptr};  // the allocations behind the field arrays
   // SAM formatting buffers (grown on demand) and the statistics accumulator
   uint64_t *d_fmtLen = nullptr, *d_fmtOff = nullptr;
   uint32_t *d_fmtIdx = nullptr, *d_fmtErr = nullptr;
@@ -471,45 +474,153 @@ void gwa_free(void *p) { free(p); }
 
 static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
-                b->d_stair, b->d_stairBase, b->d_seq, b->d_name, b->d_qual, b->d_seqOff, b->d_nameOff, b->d_qualOff,
+                b->d_stair, b->d_stairBase, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats};
   for (void *p : ps)
     if (p) (void)hipFree(p);
+  // the text blobs (one allocation may back several of them)
+  char *tx[3] = {b->d_seqText, b->d_nameText, b->d_qualText};
+  for (int i = 0; i < 3; ++i) {
+    bool dup = false;
+    for (int j = 0; j < i; ++j) dup = dup || tx[j] == tx[i];
+    if (tx[i] && !dup) (void)hipFree(tx[i]);
+  }
   if (b->stream) (void)hipStreamDestroy(b->stream);
   b->stream = nullptr;
 }
 
+}  // extern "C"
+
+// Batch set-up shared by every way reads arrive: config, stream; true for -m bd / -m bwa
+static bool batchHead(gwa_index *ix, const gwa_config_t *cfg, uint32_t n, gwa_batch *b) {
+  if (cfg->strategy < 0 || cfg->strategy > 3) throw std::runtime_error("unknown strategy (-m bsf, sf, bd, bwa)");
+  HIPCHK(hipSetDevice(ix->device));
+  b->ix = ix;
+  b->cfg = *cfg;
+  b->n = n;
+  if (cfg->strategy >= 2) {
+    // -m bd / -m bwa (A/Align.java:124-132): BidirectionalBWT reports BWAState / AlignmentSA objects,
+    // which SAMOutput.emit drops (it prints AlignmentRecord only, A/SAMOutput.java:73-82), so the
+    // reference's SAM is the header alone.  Same output here, without a search whose results no one
+    // reads.
+    b->headerOnly = true;
+    return true;
+  }
+  SearchConfig &sc = b->scfg;
+  sc.k = cfg->k; sc.reportType = cfg->report_type; sc.topL = cfg->top_l; sc.numSplit = cfg->num_split;
+  sc.matchScore = cfg->match; sc.mismatchPenalty = cfg->mismatch; sc.splitOpenPenalty = cfg->split_open;
+  sc.indelEndSkip = cfg->indel_end_skip; sc.bandWidth = cfg->band_width;
+  sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 16;
+  sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
+  sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
+  HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  return false;
+}
+
+// Once the read text is in HBM (b->d_seqText with d_seqB / d_seqE, names, qualities): encode the
+// bases on the device (batch_io.hip: ACGTSequence(String), A/ACGTSequence.java:86-97), build the
+// staircase tables of the batch's read lengths and allocate the search and output buffers.
+static void batchTail(gwa_batch *b, uint64_t seqBytes) {
+  const uint32_t n = b->n;
+  const gwa_config_t *cfg = &b->cfg;
+  hipStream_t s = b->stream;
+  const uint64_t codeBound = seqBytes + 16ull * n + 32;
+  if (codeBound > 0xFFFFFFFFull) throw std::runtime_error("read batch too large (> 4 GiB of codes): use fewer reads per batch");
+  b->d_codes = devAlloc<uint8_t>(codeBound);
+  b->d_off = devAlloc<uint32_t>((size_t)n + 1);
+  b->d_len = devAlloc<uint32_t>((size_t)n + 1);
+  uint32_t *d_row = devAlloc<uint32_t>((size_t)n + 1);
+  uint32_t *d_seen = devAlloc<uint32_t>(kLenSeen);
+  const size_t tmpBytes = encodeScanTempBytes(n);
+  void *d_tmp = devAlloc<uint8_t>(tmpBytes);
+  std::vector<uint32_t> seen(kLenSeen);
+  try {
+    HIPCHK(hipMemsetAsync(d_seen, 0, kLenSeen * sizeof(uint32_t), s));
+    launchEncode(b->d_seqText, b->d_seqB, b->d_seqE, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 0, s);
+    launchEncode(b->d_seqText, b->d_seqB, b->d_seqE, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 1, s);
+    HIPCHK(hipMemcpyAsync(seen.data(), d_seen, kLenSeen * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  } catch (...) {
+    (void)hipFree(d_row);
+    (void)hipFree(d_seen);
+    (void)hipFree(d_tmp);
+    throw;
+  }
+  (void)hipFree(d_row);
+  (void)hipFree(d_seen);
+  (void)hipFree(d_tmp);
+  // the distinct read lengths: maximum length, k per length (AlignmentScoreConfig
+  // .getMaximumEditDistance) and the staircase tables
+  std::vector<int> lens;
+  for (uint32_t m = 0; m < kLenSeen; ++m)
+    if (seen[m]) {
+      b->maxM = (int)m;
+      if (m <= 255) lens.push_back((int)m);
+    }
+  for (int m : lens) {
+    int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
+    b->kmax = std::max(b->kmax, k);
+  }
+  if (b->kmax > 31) throw std::runtime_error("k > 31 is not supported on the device path");
+  b->R = b->kmax + 1 <= 4 ? 4 : b->kmax + 1 <= 8 ? 8 : b->kmax + 1 <= 16 ? 16 : 32;
+  std::vector<uint64_t> tab;
+  std::vector<uint32_t> base;
+  buildStairTables(lens, std::max(b->kmax, 0), tab, base);
+  b->d_stair = devUpload(tab, s, nullptr);
+  b->d_stairBase = devUpload(base, s, nullptr);
+  b->st.tab = b->d_stair;
+  b->st.base = b->d_stairBase;
+  b->st.kmax = std::max(b->kmax, 0);
+  b->st.ldsM = -1;
+  {  // stage the table of the longest length in LDS when it fits (all reads share it in the usual case)
+    const int km = std::max(b->kmax, 0), m0 = b->maxM;
+    const uint64_t cnt = (uint64_t)(km + 2) * (km + 1) * (uint64_t)(m0 + km + 1);
+    if (m0 >= 1 && m0 <= 255 && base[(size_t)m0] < 0xFFFFFFFEu && cnt <= (uint64_t)kStairLdsWords) {
+      b->st.ldsM = m0;
+      b->st.ldsBase = base[(size_t)m0];
+      b->st.ldsCount = (uint32_t)cnt;
+    }
+  }
+  // fixed output slot per read: the chains besthit / a small -L report; more go to the pool
+  const int chains = cfg->report_type == 0 ? 1 : cfg->report_type == 2 ? std::max(1, std::min(cfg->top_l, 4)) : 2;
+  b->hitCap = (uint32_t)(chains * std::max(1, cfg->num_split + 1));
+  b->cigCap = (uint32_t)(64 * chains);
+  b->poolHits = std::max<uint64_t>(1 << 16, (uint64_t)n * b->hitCap / 16);
+  b->poolCig = std::max<uint64_t>(1 << 20, (uint64_t)n * b->cigCap / 16);
+  if (const char *e = getenv("GWA_OUT_POOL")) {  // initial pool size in hits (tests: force growth)
+    b->poolHits = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    b->poolCig = 64 * b->poolHits;
+  }
+  if ((uint64_t)n * b->cigCap + b->poolCig >= 0xFFFFFFFFull)
+    throw std::runtime_error("read batch too large for 32-bit output offsets: use fewer reads per batch");
+  b->d_sres = devAlloc<ScanRes>(n);
+  b->d_oh = devAlloc<OutHeader>(n);
+  b->d_hits = devAlloc<OutHit>((size_t)n * b->hitCap + b->poolHits);
+  b->d_cig = devAlloc<uint16_t>((size_t)n * b->cigCap + b->poolCig);
+  b->d_list[0] = devAlloc<uint32_t>(n);
+  b->d_list[1] = devAlloc<uint32_t>(n);
+  b->d_count = devAlloc<uint32_t>(16);
+  if (cfg->strategy == 1) {
+    std::vector<uint32_t> all(n);
+    for (uint32_t i = 0; i < n; ++i) all[i] = i;
+    b->d_all = devUpload(all, s, nullptr);
+  }
+  HIPCHK(hipStreamSynchronize(s));
+}
+
+extern "C" {
+
 int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_batch_t **out) {
   auto *b = new gwa_batch();
   try {
-    if (cfg->strategy < 0 || cfg->strategy > 3) throw std::runtime_error("unknown strategy (-m bsf, sf, bd, bwa)");
-    HIPCHK(hipSetDevice(ix->device));
-    b->ix = ix;
-    b->cfg = *cfg;
-    if (cfg->strategy >= 2) {
-      // -m bd / -m bwa (A/Align.java:124-132): BidirectionalBWT reports BWAState / AlignmentSA objects,
-      // which SAMOutput.emit drops (it prints AlignmentRecord only, A/SAMOutput.java:73-82), so the
-      // reference's SAM is the header alone.  Same output here, without a search whose results no one
-      // reads.
-      b->headerOnly = true;
-      b->n = reads->n;
+    const uint32_t n = reads->n;
+    if (batchHead(ix, cfg, n, b)) {
       *out = b;
       return 0;
     }
-    SearchConfig &sc = b->scfg;
-    sc.k = cfg->k; sc.reportType = cfg->report_type; sc.topL = cfg->top_l; sc.numSplit = cfg->num_split;
-    sc.matchScore = cfg->match; sc.mismatchPenalty = cfg->mismatch; sc.splitOpenPenalty = cfg->split_open;
-    sc.indelEndSkip = cfg->indel_end_skip; sc.bandWidth = cfg->band_width;
-    sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 16;
-    sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
-    sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
-    const uint32_t n = reads->n;
-    b->n = n;
     b->hasQual = reads->qual != nullptr;
-    HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
     hipStream_t s = b->stream;
-    // the read text goes to HBM as it is (offsets rebased to the blob starts) and is encoded there
-    // (batch_io.hip: ACGTSequence(String), A/ACGTSequence.java:86-97)
+    // the read text goes to HBM as it is (offsets rebased to the blob starts)
     auto blob = [&](const char *base, const uint64_t *off, char **dText, uint64_t **dOff) {
       std::vector<uint64_t> o(off, off + n + 1);
       const uint64_t o0 = o[0];
@@ -520,91 +631,22 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
       HIPCHK(hipStreamSynchronize(s));  // (o is a local vector)
       return o[n];
     };
-    const uint64_t seqBytes = blob(reads->seq, reads->seq_off, &b->d_seq, &b->d_seqOff);
-    blob(reads->name, reads->name_off, &b->d_name, &b->d_nameOff);
-    if (b->hasQual) blob(reads->qual, reads->qual_off, &b->d_qual, &b->d_qualOff);
-    const uint64_t codeBound = seqBytes + 16ull * n + 32;
-    if (codeBound > 0xFFFFFFFFull) throw std::runtime_error("read batch too large (> 4 GiB of codes): use fewer reads per batch");
-    b->d_codes = devAlloc<uint8_t>(codeBound);
-    b->d_off = devAlloc<uint32_t>((size_t)n + 1);
-    b->d_len = devAlloc<uint32_t>((size_t)n + 1);
-    uint32_t *d_row = devAlloc<uint32_t>((size_t)n + 1);
-    uint32_t *d_seen = devAlloc<uint32_t>(kLenSeen);
-    const size_t tmpBytes = encodeScanTempBytes(n);
-    void *d_tmp = devAlloc<uint8_t>(tmpBytes);
-    std::vector<uint32_t> seen(kLenSeen);
-    try {
-      HIPCHK(hipMemsetAsync(d_seen, 0, kLenSeen * sizeof(uint32_t), s));
-      launchEncode(b->d_seq, b->d_seqOff, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 0, s);
-      launchEncode(b->d_seq, b->d_seqOff, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 1, s);
-      HIPCHK(hipMemcpyAsync(seen.data(), d_seen, kLenSeen * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-    } catch (...) {
-      (void)hipFree(d_row);
-      (void)hipFree(d_seen);
-      (void)hipFree(d_tmp);
-      throw;
+    uint64_t *off = nullptr;
+    const uint64_t seqBytes = blob(reads->seq, reads->seq_off, &b->d_seqText, &off);
+    b->d_fieldOwn[0] = off;
+    b->d_seqB = off;
+    b->d_seqE = off + 1;
+    blob(reads->name, reads->name_off, &b->d_nameText, &off);
+    b->d_fieldOwn[1] = off;
+    b->d_nameB = off;
+    b->d_nameE = off + 1;
+    if (b->hasQual) {
+      blob(reads->qual, reads->qual_off, &b->d_qualText, &off);
+      b->d_fieldOwn[2] = off;
+      b->d_qualB = off;
+      b->d_qualE = off + 1;
     }
-    (void)hipFree(d_row);
-    (void)hipFree(d_seen);
-    (void)hipFree(d_tmp);
-    // the distinct read lengths: maximum length, k per length (AlignmentScoreConfig
-    // .getMaximumEditDistance) and the staircase tables
-    std::vector<int> lens;
-    for (uint32_t m = 0; m < kLenSeen; ++m)
-      if (seen[m]) {
-        b->maxM = (int)m;
-        if (m <= 255) lens.push_back((int)m);
-      }
-    for (int m : lens) {
-      int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
-      b->kmax = std::max(b->kmax, k);
-    }
-    if (b->kmax > 31) throw std::runtime_error("k > 31 is not supported on the device path");
-    b->R = b->kmax + 1 <= 4 ? 4 : b->kmax + 1 <= 8 ? 8 : b->kmax + 1 <= 16 ? 16 : 32;
-    std::vector<uint64_t> tab;
-    std::vector<uint32_t> base;
-    buildStairTables(lens, std::max(b->kmax, 0), tab, base);
-    b->d_stair = devUpload(tab, s, nullptr);
-    b->d_stairBase = devUpload(base, s, nullptr);
-    b->st.tab = b->d_stair;
-    b->st.base = b->d_stairBase;
-    b->st.kmax = std::max(b->kmax, 0);
-    b->st.ldsM = -1;
-    {  // stage the table of the longest length in LDS when it fits (all reads share it in the usual case)
-      const int km = std::max(b->kmax, 0), m0 = b->maxM;
-      const uint64_t cnt = (uint64_t)(km + 2) * (km + 1) * (uint64_t)(m0 + km + 1);
-      if (m0 >= 1 && m0 <= 255 && base[(size_t)m0] < 0xFFFFFFFEu && cnt <= (uint64_t)kStairLdsWords) {
-        b->st.ldsM = m0;
-        b->st.ldsBase = base[(size_t)m0];
-        b->st.ldsCount = (uint32_t)cnt;
-      }
-    }
-    // fixed output slot per read: the chains besthit / a small -L report; more go to the pool
-    const int chains = cfg->report_type == 0 ? 1 : cfg->report_type == 2 ? std::max(1, std::min(cfg->top_l, 4)) : 2;
-    b->hitCap = (uint32_t)(chains * std::max(1, cfg->num_split + 1));
-    b->cigCap = (uint32_t)(64 * chains);
-    b->poolHits = std::max<uint64_t>(1 << 16, (uint64_t)n * b->hitCap / 16);
-    b->poolCig = std::max<uint64_t>(1 << 20, (uint64_t)n * b->cigCap / 16);
-    if (const char *e = getenv("GWA_OUT_POOL")) {  // initial pool size in hits (tests: force growth)
-      b->poolHits = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
-      b->poolCig = 64 * b->poolHits;
-    }
-    if ((uint64_t)n * b->cigCap + b->poolCig >= 0xFFFFFFFFull)
-      throw std::runtime_error("read batch too large for 32-bit output offsets: use fewer reads per batch");
-    b->d_sres = devAlloc<ScanRes>(n);
-    b->d_oh = devAlloc<OutHeader>(n);
-    b->d_hits = devAlloc<OutHit>((size_t)n * b->hitCap + b->poolHits);
-    b->d_cig = devAlloc<uint16_t>((size_t)n * b->cigCap + b->poolCig);
-    b->d_list[0] = devAlloc<uint32_t>(n);
-    b->d_list[1] = devAlloc<uint32_t>(n);
-    b->d_count = devAlloc<uint32_t>(16);
-    if (cfg->strategy == 1) {
-      std::vector<uint32_t> all(n);
-      for (uint32_t i = 0; i < n; ++i) all[i] = i;
-      b->d_all = devUpload(all, s, nullptr);
-    }
-    HIPCHK(hipStreamSynchronize(s));
+    batchTail(b, seqBytes);
     *out = b;
     return 0;
   } catch (std::exception &e) {
@@ -613,6 +655,67 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
     return fail(e.what());
   }
 }
+
+}  // extern "C"
+
+namespace gwa {
+// Pipeline use (pipeline.cpp): a batch from FASTQ text holding n complete records, record r's header
+// line at start[r] (reads_io.cpp frameRecords).  The text goes to HBM as it is and the record fields
+// are located there (batch_io.hip fastqFieldsKernel); names and qualities are read by the SAM writer
+// in place.  A malformed record fails with the host parser's message.
+int batchCreateFastq(gwa_index_t *ix, const gwa_config_t *cfg, const char *text, uint64_t len, const uint64_t *start,
+                     uint32_t n, gwa_batch_t **out) {
+  auto *b = new gwa_batch();
+  try {
+    if (batchHead(ix, cfg, n, b)) {
+      *out = b;
+      return 0;
+    }
+    b->hasQual = true;
+    hipStream_t s = b->stream;
+    char *dText = devAlloc<char>(len + 1);
+    b->d_seqText = dText;
+    HIPCHK(hipMemcpyAsync(dText, text, len, hipMemcpyHostToDevice, s));
+    uint64_t *dStart = devAlloc<uint64_t>(n);
+    HIPCHK(hipMemcpyAsync(dStart, start, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    uint64_t *f = devAlloc<uint64_t>(6 * (size_t)n);
+    b->d_fieldOwn[0] = f;
+    uint32_t *dErr = devAlloc<uint32_t>(1);
+    uint32_t err = 0;
+    HIPCHK(hipMemsetAsync(dErr, 0xFF, 4, s));
+    launchFastqFields(dText, len, dStart, n, f, dErr, s);
+    HIPCHK(hipMemcpyAsync(&err, dErr, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    (void)hipFree(dStart);
+    (void)hipFree(dErr);
+    if (err != 0xFFFFFFFFu) {  // the host parser words the error
+      gwa_read_buf_t pb{};
+      uint64_t used = 0;
+      if (gwa_reads_parse(text, len, 1, 1, &pb, &used) != 0) throw std::runtime_error(gwa_last_error());
+      gwa_reads_free(&pb);
+      throw std::runtime_error("malformed FASTQ record " + std::to_string(err));
+    }
+    b->d_nameText = dText;
+    b->d_qualText = dText;
+    b->d_nameB = f;
+    b->d_nameE = f + n;
+    b->d_seqB = f + 2 * (size_t)n;
+    b->d_seqE = f + 3 * (size_t)n;
+    b->d_qualB = f + 4 * (size_t)n;
+    b->d_qualE = f + 5 * (size_t)n;
+    uint64_t seqBytes = len;  // (an upper bound of the bases: the codes buffer is sized from it)
+    batchTail(b, seqBytes);
+    *out = b;
+    return 0;
+  } catch (std::exception &e) {
+    freeBatchDev(b);
+    delete b;
+    return fail(e.what());
+  }
+}
+}  // namespace gwa
+
+extern "C" {
 
 // capacity tiers: (arena, heap, hits, list, cigar, candidates) and the lane budget of each tier
 struct Tier {
@@ -851,10 +954,12 @@ static void ensureStats(gwa_batch *b) {
 
 static SamText samText(const gwa_batch *b) {
   SamText t;
-  t.name = b->d_name;
-  t.nameOff = b->d_nameOff;
-  t.qual = b->hasQual ? b->d_qual : nullptr;
-  t.qualOff = b->d_qualOff;
+  t.name = b->d_nameText;
+  t.nameB = b->d_nameB;
+  t.nameE = b->d_nameE;
+  t.qual = b->hasQual ? b->d_qualText : nullptr;
+  t.qualB = b->d_qualB;
+  t.qualE = b->d_qualE;
   t.codes = b->d_codes;
   t.codeOff = b->d_off;
   t.codeLen = b->d_len;
@@ -876,19 +981,10 @@ static void growDev(T **p, size_t *cap, size_t need) {
 }
 
 // SAM text of the reads idx[0..count) (or first .. first + count - 1) written on the device
-// (batch_io.hip), copied to library-owned host memory in one piece
-static void formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t first, uint32_t count, gwa_results_t *out) {
+// (batch_io.hip) into d_fmtText, line offsets in d_fmtOff; returns the text size in bytes
+static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t first, uint32_t count) {
   if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
   const uint32_t n = count;
-  out->n_reads = n;
-  out->sam = nullptr;
-  out->line_off = nullptr;
-  if (b->headerOnly) {
-    out->sam = (char *)calloc(1, 1);
-    out->sam_len = 0;
-    out->line_off = (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t));
-    return;
-  }
   HIPCHK(hipSetDevice(b->ix->device));
   hipStream_t s = b->stream;
   if (!b->d_fmtLen || b->fmtCap < (size_t)n + 1) {
@@ -928,9 +1024,10 @@ static void formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t first
     OutHeader h;
     uint64_t no[2];
     HIPCHK(hipMemcpy(&h, b->d_oh + r, sizeof(h), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(no, b->d_nameOff + r, sizeof(no), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&no[0], b->d_nameB + r, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&no[1], b->d_nameE + r, 8, hipMemcpyDeviceToHost));
     std::string nm(no[1] - no[0], '\0');
-    if (!nm.empty()) HIPCHK(hipMemcpy(&nm[0], b->d_name + no[0], nm.size(), hipMemcpyDeviceToHost));
+    if (!nm.empty()) HIPCHK(hipMemcpy(&nm[0], b->d_nameText + no[0], nm.size(), hipMemcpyDeviceToHost));
     const int stt = h.status;
     throw std::runtime_error(std::string(stt == ST_TOO_LONG ? "read longer than the device path supports: "
                                          : stt == ST_OVERFLOW ? "output slot overflow at read "
@@ -940,6 +1037,24 @@ static void formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t first
   growDev(&b->d_fmtText, &b->fmtTextCap, (size_t)total + 1);
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
                   b->d_fmtErr, b->d_fmtText, 2, s);
+  return total;
+}
+
+// formatOnDevice into library-owned host memory (gwa_results_t)
+static void formatResults(gwa_batch *b, const uint32_t *hostIdx, uint32_t first, uint32_t count, gwa_results_t *out) {
+  const uint32_t n = count;
+  out->n_reads = n;
+  out->sam = nullptr;
+  out->line_off = nullptr;
+  if (b->headerOnly) {
+    if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
+    out->sam = (char *)calloc(1, 1);
+    out->sam_len = 0;
+    out->line_off = (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t));
+    return;
+  }
+  const uint64_t total = formatOnDevice(b, hostIdx, first, count);
+  hipStream_t s = b->stream;
   out->sam = (char *)malloc(total + 1);
   out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n + 1));
   if (!out->sam || !out->line_off) {
@@ -955,6 +1070,32 @@ static void formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t first
   out->sam[total] = 0;
   out->sam_len = total;
 }
+
+namespace gwa {
+// Pipeline use (pipeline.cpp): the whole batch's SAM text into a caller buffer (pinned host memory,
+// grown with hipHostMalloc as needed); returns its size.  Throws on a failing read.
+uint64_t batchSamInto(gwa_batch_t *b, char **buf, uint64_t *cap) {
+  if (b->headerOnly) {
+    if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
+    return 0;
+  }
+  const uint64_t total = formatOnDevice(b, nullptr, 0, b->n);
+  if (*cap < total) {
+    if (*buf) (void)hipHostFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    const uint64_t want = total + total / 8 + (1 << 20);
+    HIPCHK(hipHostMalloc((void **)buf, want, hipHostMallocDefault));
+    *cap = want;
+  }
+  if (total) HIPCHK(hipMemcpyAsync(*buf, b->d_fmtText, total, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return total;
+}
+void pinnedFree(char *p) {
+  if (p) (void)hipHostFree(p);
+}
+}  // namespace gwa
 
 extern "C" {
 
@@ -973,7 +1114,7 @@ int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) { return gwa_batch_res
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out) {
   try {
     if ((uint64_t)first + count > b->n) throw std::runtime_error("result range out of bounds");
-    formatOnDevice(b, nullptr, first, count, out);
+    formatResults(b, nullptr, first, count, out);
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());
@@ -984,7 +1125,7 @@ int gwa_batch_results_select(gwa_batch_t *b, const uint32_t *idx, uint32_t count
   try {
     for (uint32_t j = 0; j < count; ++j)
       if (idx[j] >= b->n) throw std::runtime_error("result index out of bounds");
-    formatOnDevice(b, idx, 0, count, out);
+    formatResults(b, idx, 0, count, out);
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());

@@ -28,9 +28,11 @@ void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream
 struct SamText;
 constexpr uint32_t kLenSeen = 65536;  // read-length presence table (lengths >= 65535 share the last slot)
 constexpr int kStatFields = 14;
-void launchEncode(const char *seq, const uint64_t *seqOff, uint32_t n, uint32_t *codeLen, uint32_t *rowLen,
-                  uint32_t *codeOff, uint32_t *lenSeen, uint8_t *codes, void *scanTmp, size_t scanTmpBytes, int pass,
-                  hipStream_t s);
+void launchEncode(const char *seq, const uint64_t *seqB, const uint64_t *seqE, uint32_t n, uint32_t *codeLen,
+                  uint32_t *rowLen, uint32_t *codeOff, uint32_t *lenSeen, uint8_t *codes, void *scanTmp,
+                  size_t scanTmpBytes, int pass, hipStream_t s);
+void launchFastqFields(const char *text, uint64_t len, const uint64_t *start, uint32_t n, uint64_t *fields,
+                       uint32_t *err, hipStream_t s);
 size_t encodeScanTempBytes(uint32_t n);
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
                      uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,

@@ -12,6 +12,7 @@
 // and the caller, which writes the results in batch order.  With two workers per device, one
 // worker's set-up and SAM formatting overlap the other's kernels (gwa_index serialises the kernels
 // of its batches, gwa_api.cpp runMu).  At most `depth` batches are in flight, which bounds memory.
+#include <hip/hip_runtime.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -29,6 +30,8 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <vector>
 
@@ -37,7 +40,17 @@
 extern "C" int gwa_fail_message(const char *msg);  // gwa_api.cpp
 
 namespace gwa {
-uint64_t frameRecords(const char *t, uint64_t len, int format, bool final, uint64_t maxRec, uint64_t *nRec);
+uint64_t frameRecords(const char *t, uint64_t len, int format, bool final, uint64_t maxRec, uint64_t *nRec,
+                      std::vector<uint64_t> *starts);
+void newlinePositions(const char *t, uint64_t a, uint64_t b, std::vector<uint64_t> &out);
+void newlineCount(const char *t, uint64_t a, uint64_t b, uint64_t *count, bool *blank, bool *cr);
+void recordStartsFromNewlines(const char *t, uint64_t a, uint64_t b, uint64_t g0, uint64_t *starts, uint64_t cap);
+uint64_t frameFastqLines(const char *t, uint64_t len, const std::vector<uint64_t> &nl, bool final, uint64_t maxRec,
+                         uint64_t *nRec, std::vector<uint64_t> *starts);
+int batchCreateFastq(gwa_index_t *ix, const gwa_config_t *cfg, const char *text, uint64_t len, const uint64_t *start,
+                     uint32_t n, gwa_batch_t **out);
+uint64_t batchSamInto(gwa_batch_t *b, char **buf, uint64_t *cap);  // gwa_api.cpp
+void pinnedFree(char *p);
 }
 
 namespace {
@@ -45,14 +58,62 @@ namespace {
 using Clock = std::chrono::steady_clock;
 double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
+// A buffer of read-file text; buffers are recycled through a pool when the last job that
+// references one is done (no zero-fill, no page faults after the first use).
+struct TextBuf {
+  char *p = nullptr;
+  size_t cap = 0, size = 0;
+  const char *data() const { return p; }
+};
+
+class BufPool {
+  std::mutex mu;
+  std::vector<TextBuf *> free_;
+
+ public:
+  ~BufPool() {
+    for (auto *b : free_) {
+      ::free(b->p);
+      delete b;
+    }
+  }
+  std::shared_ptr<TextBuf> get(size_t cap) {
+    TextBuf *b = nullptr;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i]->cap >= cap) {
+          b = free_[i];
+          free_.erase(free_.begin() + (long)i);
+          break;
+        }
+    }
+    if (!b) {
+      b = new TextBuf();
+      b->p = (char *)::malloc(cap);
+      if (!b->p) {
+        delete b;
+        throw std::runtime_error("out of host memory for the read text");
+      }
+      b->cap = cap;
+    }
+    b->size = 0;
+    return std::shared_ptr<TextBuf>(b, [this](TextBuf *x) {
+      std::lock_guard<std::mutex> g(mu);
+      free_.push_back(x);
+    });
+  }
+};
+
 // One unit of work: either reads already in memory (a gwa_reads_t slice) or a framed slice of file
 // text that the worker parses itself.
 struct Job {
   uint64_t id = 0;
   gwa_reads_t reads{};                 // in-memory reads (text == nullptr)
-  std::shared_ptr<std::string> text;   // or: file text holding complete records [tb, te)
+  std::shared_ptr<TextBuf> text;       // or: file text holding complete records [tb, te)
   uint64_t tb = 0, te = 0;
   int format = 1;
+  std::vector<uint64_t> starts;  // FASTQ: each record's header line, relative to tb
 };
 
 struct Result {
@@ -85,6 +146,17 @@ struct Run {
   std::vector<std::thread> workers;
   std::atomic<uint64_t> reads{0};
   std::vector<double> devBusy;  // per device: seconds of kernels
+  double parseS = 0, setupS = 0, formatS = 0, writeS = 0, waitS = 0;  // summed over worker threads
+  // file mode: each worker writes its own batch's SAM from its pinned buffer -- at its offset with
+  // pwrite when the output is a regular file (offsets fixed in batch order as sizes become known),
+  // else in batch order with write
+  int fd = -1;
+  bool seekable = false;
+  uint64_t base = 0;                        // file position of the first record
+  std::map<uint64_t, uint64_t> sizes, offs; // batch -> SAM bytes / offset
+  uint64_t cursor = 0, nextOff = 0;         // first batch whose offset is not fixed yet, its offset
+  uint64_t turn = 0;                        // non-seekable output: the batch that writes next
+  std::atomic<uint64_t> fileReads{0}, fileBatches{0};
 
   explicit Run(gwa_pipeline *p_) : p(p_) {
     depth = std::max<size_t>(4, 2 * p->ix.size() * p->workersPerDevice);
@@ -163,6 +235,118 @@ struct Run {
     }
   }
 
+  // file mode: put batch `id`'s SAM (size bytes at p) into the output in batch order
+  void output(uint64_t id, const char *p, uint64_t size) {
+    const auto w0 = Clock::now();
+    uint64_t off = 0;
+    {
+      std::unique_lock<std::mutex> g(mu);
+      if (seekable) {
+        sizes[id] = size;
+        for (auto it = sizes.find(cursor); it != sizes.end(); it = sizes.find(cursor)) {
+          offs[cursor] = nextOff;
+          nextOff += it->second;
+          sizes.erase(it);
+          ++cursor;
+        }
+        cv.notify_all();
+        cv.wait(g, [&] { return failed || offs.count(id) != 0; });
+        if (failed) return;
+        off = offs[id];
+        offs.erase(id);
+      } else {
+        cv.wait(g, [&] { return failed || turn == id; });
+        if (failed) return;
+      }
+    }
+    const auto w1 = Clock::now();
+    uint64_t done = 0;
+    while (done < size) {
+      const size_t chunk = (size_t)std::min<uint64_t>(size - done, 1ull << 30);
+      const ssize_t w = seekable ? ::pwrite(fd, p + done, chunk, (off_t)(base + off + done)) : ::write(fd, p + done, chunk);
+      if (w <= 0) throw std::runtime_error("write to the SAM output failed");
+      done += (uint64_t)w;
+    }
+    const auto w2 = Clock::now();
+    std::lock_guard<std::mutex> g(mu);
+    if (!seekable) ++turn;
+    waitS += secs(w0, w1);
+    writeS += secs(w1, w2);
+    cv.notify_all();
+  }
+
+  // file mode worker: parse its framed slice, align it on device d, write its SAM
+  void fileWorker(int d) {
+    gwa_index_t *ix = p->ix[(size_t)d];
+    char *pinned = nullptr;
+    uint64_t cap = 0;
+    try {
+      for (;;) {
+        Job j;
+        {
+          std::unique_lock<std::mutex> g(mu);
+          cv.wait(g, [&] { return failed || !jobs.empty() || noMoreJobs; });
+          if (failed || jobs.empty()) break;
+          j = std::move(jobs.front());
+          jobs.pop_front();
+        }
+        const auto t0 = Clock::now();
+        gwa_batch_t *b = nullptr;
+        int rc = 0;
+        uint32_t nr = 0;
+        auto t1 = t0;
+        if (j.format == 1) {  // FASTQ: the text itself goes to the device, fields located there
+          nr = (uint32_t)j.starts.size();
+          rc = gwa::batchCreateFastq(ix, &p->cfg, j.text->data() + j.tb, j.te - j.tb, j.starts.data(), nr, &b);
+        } else {  // FASTA reads (multi-line records): parsed on the host
+          gwa_read_buf_t parsed{};
+          uint64_t used = 0;
+          if (gwa_reads_parse(j.text->data() + j.tb, j.te - j.tb, j.format, 1, &parsed, &used) != 0)
+            throw std::runtime_error(gwa_last_error());
+          t1 = Clock::now();
+          nr = parsed.reads.n;
+          rc = gwa_batch_create(ix, &p->cfg, &parsed.reads, &b);
+          gwa_reads_free(&parsed);
+        }
+        j.text.reset();
+        const auto t2 = Clock::now();
+        if (rc == 0) rc = gwa_batch_run(b);
+        const auto t3 = Clock::now();
+        uint64_t size = 0;
+        if (rc == 0) {
+          try {
+            size = gwa::batchSamInto(b, &pinned, &cap);
+          } catch (...) {
+            gwa_batch_free(b);
+            throw;
+          }
+        }
+        const std::string msg = rc != 0 ? std::string(gwa_last_error()) : std::string();
+        gwa_batch_free(b);
+        if (rc != 0) throw std::runtime_error("batch " + std::to_string(j.id) + ": " + msg);
+        const auto t4 = Clock::now();
+        output(j.id, pinned, size);
+        fileReads += nr;
+        ++fileBatches;
+        std::lock_guard<std::mutex> g(mu);
+        parseS += secs(t0, t1);
+        setupS += secs(t1, t2);
+        devBusy[(size_t)d] += secs(t2, t3);
+        formatS += secs(t3, t4);
+        --inflight;
+        cv.notify_all();
+      }
+    } catch (std::exception &e) {
+      fail(e.what());
+    }
+    gwa::pinnedFree(pinned);
+  }
+
+  void startFile() {
+    for (int w = 0; w < p->workersPerDevice; ++w)
+      for (size_t d = 0; d < p->ix.size(); ++d) workers.emplace_back(&Run::fileWorker, this, (int)d);
+  }
+
   void start() {
     for (int w = 0; w < p->workersPerDevice; ++w)
       for (size_t d = 0; d < p->ix.size(); ++d) workers.emplace_back(&Run::worker, this, (int)d);
@@ -189,15 +373,6 @@ struct Run {
     done.clear();
   }
 };
-
-void writeAll(int fd, const char *p, uint64_t n) {
-  while (n > 0) {
-    const ssize_t w = ::write(fd, p, (size_t)std::min<uint64_t>(n, 1ull << 30));
-    if (w < 0) throw std::runtime_error("write to the SAM output failed");
-    p += w;
-    n -= (uint64_t)w;
-  }
-}
 
 int formatOf(const char *path) {
   std::string s(path);
@@ -288,6 +463,7 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
     }
     out->line_off[n] = pos;
     out->sam[total] = 0;
+    p->stats = gwa_pipeline_stats_t{};
     p->stats.reads = n;
     p->stats.batches = nb;
     p->stats.wall_s = secs(t0, Clock::now());
@@ -302,103 +478,273 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
 }
 
 int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_t *n_reads) {
+  BufPool pool;  // (outlives every job that holds one of its buffers)
   Run run(p);
+  gzFile f = nullptr;
+  int in = -1;
   try {
     const int fmt = formatOf(path);
-    gzFile f = gzopen(path, "rb");
-    if (!f) throw std::runtime_error(std::string("cannot open ") + path);
-    gzbuffer(f, 1u << 20);
+    const bool gz = strlen(path) > 3 && strcmp(path + strlen(path) - 3, ".gz") == 0;
+    if (gz) {
+      f = gzopen(path, "rb");
+      if (!f) throw std::runtime_error(std::string("cannot open ") + path);
+      gzbuffer(f, 1u << 20);
+    } else {
+      in = ::open(path, O_RDONLY);
+      if (in < 0) throw std::runtime_error(std::string("cannot open ") + path);
+    }
+    struct stat sb;
+    const off_t pos0 = ::lseek(fd, 0, SEEK_CUR);
+    run.fd = fd;
+    run.seekable = pos0 >= 0 && ::fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+    run.base = run.seekable ? (uint64_t)pos0 : 0;
     const auto t0 = Clock::now();
-    double readS = 0;
-    run.start();
-    std::atomic<uint64_t> nJobs{0};
-    std::atomic<bool> readerDone{false};
-    std::string readErr;
-    std::thread reader([&] {
+    double readS = 0, frameS = 0;
+    run.startFile();
+    // This thread reads the file and frames it into batches of complete records (FASTQ: every
+    // record's header offset, from the '\n' positions found on several threads); the workers do the
+    // rest.  Only full batches leave a chunk unless the file has ended; the rest carries over.
+    // An IO thread reads the file in chunks into pooled pinned buffers, behind `reserve` bytes of
+    // room where this thread puts the records carried over from the previous chunk; this thread frames
+    // each chunk into batches of complete records (FASTQ: every record's header offset) while the IO
+    // thread reads the next.  Only full batches leave a chunk unless the file has ended.
+    const uint64_t chunk = 256ull << 20;
+    const uint64_t reserve = 512ull << 20;
+    const unsigned nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    struct Chunk {
+      std::shared_ptr<TextBuf> buf;
+      uint64_t got = 0;
+      bool final = false;
+    };
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::deque<Chunk> q;
+    bool ioDone = false, stop = false;
+    std::string ioErr;
+    std::thread io([&] {
       try {
-        const uint64_t chunk = 256ull << 20;
-        std::string carry;
-        uint64_t id = 0;
         for (;;) {
-          auto buf = std::make_shared<std::string>();
-          buf->swap(carry);
-          const size_t old = buf->size();
-          buf->resize(old + chunk);
+          {
+            std::unique_lock<std::mutex> g(qmu);
+            qcv.wait(g, [&] { return stop || q.size() < 2; });
+            if (stop) break;
+          }
+          Chunk c;
+          c.buf = pool.get(reserve + chunk);
           const auto r0 = Clock::now();
-          const int got = gzread(f, &(*buf)[old], (unsigned)chunk);
-          readS += secs(r0, Clock::now());
-          if (got < 0) throw std::runtime_error(std::string("read error: ") + path);
-          buf->resize(old + (size_t)got);
-          const bool final = got == 0;
-          uint64_t pos = 0;
-          while (pos < buf->size()) {
-            uint64_t nrec = 0;
-            const uint64_t e = pos + gwa::frameRecords(buf->data() + pos, buf->size() - pos, fmt, final, p->batchReads, &nrec);
-            if (nrec == 0) {
-              if (final) pos = buf->size();  // trailing text without records
-              break;
+          char *dst = c.buf->p + reserve;
+          if (gz) {
+            while (c.got < chunk) {
+              const int r = gzread(f, dst + c.got, (unsigned)(chunk - c.got));
+              if (r < 0) throw std::runtime_error(std::string("read error: ") + path);
+              if (r == 0) break;
+              c.got += (uint64_t)r;
             }
-            if (nrec < p->batchReads && !final) break;  // wait for more text: full batches only
+          } else {  // four preads at a time (the page cache copies in parallel)
+            const off_t at = ::lseek(in, 0, SEEK_CUR);
+            std::atomic<bool> bad{false};
+            std::vector<std::thread> th;
+            const uint64_t part = chunk / 4;
+            std::vector<uint64_t> gotk(4, 0);
+            for (int k = 0; k < 4; ++k)
+              th.emplace_back([&, k] {
+                uint64_t gk = 0;
+                while (gk < part) {
+                  const ssize_t r = ::pread(in, dst + k * part + gk, (size_t)(part - gk), at + (off_t)(k * part + gk));
+                  if (r < 0) { bad = true; return; }
+                  if (r == 0) break;
+                  gk += (uint64_t)r;
+                }
+                gotk[(size_t)k] = gk;
+              });
+            for (auto &x : th) x.join();
+            if (bad) throw std::runtime_error(std::string("read error: ") + path);
+            // the bytes read are contiguous up to the first short part (end of file)
+            for (int k = 0; k < 4; ++k) {
+              c.got += gotk[(size_t)k];
+              if (gotk[(size_t)k] < part) break;
+            }
+            ::lseek(in, at + (off_t)c.got, SEEK_SET);
+          }
+          c.final = c.got < chunk;
+          const double rs = secs(r0, Clock::now());
+          std::lock_guard<std::mutex> g(qmu);
+          readS += rs;
+          const bool fin = c.final;
+          q.push_back(std::move(c));
+          qcv.notify_all();
+          if (fin) break;
+        }
+      } catch (std::exception &e) {
+        std::lock_guard<std::mutex> g(qmu);
+        ioErr = e.what();
+      }
+      std::lock_guard<std::mutex> g(qmu);
+      ioDone = true;
+      qcv.notify_all();
+    });
+    std::shared_ptr<TextBuf> prev;
+    uint64_t carryFrom = 0, carryLen = 0, id = 0;
+    bool ok = true;
+    std::vector<uint64_t> starts;
+    try {
+      for (;;) {
+        Chunk c;
+        {
+          std::unique_lock<std::mutex> g(qmu);
+          qcv.wait(g, [&] { return !q.empty() || ioDone; });
+          if (q.empty()) {
+            if (!ioErr.empty()) throw std::runtime_error(ioErr);
+            break;
+          }
+          c = std::move(q.front());
+          q.pop_front();
+          qcv.notify_all();
+        }
+        const auto f0 = Clock::now();
+        // the text of this round: the carried records, then the chunk
+        std::shared_ptr<TextBuf> buf = c.buf;
+        uint64_t base = reserve - carryLen;
+        if (carryLen > reserve) {  // more carry than room: one buffer holding both
+          buf = pool.get(carryLen + c.got + 64);
+          memcpy(buf->p + carryLen, c.buf->p + reserve, c.got);
+          base = 0;
+        }
+        if (carryLen) memcpy(buf->p + base, prev->p + carryFrom, carryLen);
+        prev.reset();
+        const char *t = buf->p + base;
+        const uint64_t len = carryLen + c.got;
+        buf->size = base + len;
+        const bool final = c.final;
+        // all complete records of the text: their header offsets (FASTQ) and the end of the last
+        starts.clear();
+        uint64_t nrec = 0, done = 0;
+        bool fast = false;
+        if (fmt == 1 && !final) {  // no '\r', no blank line: record k starts after newline 4k - 1
+          std::vector<uint64_t> cnt(nth);
+          std::vector<char> bl(nth), cr(nth);
+          std::vector<std::thread> th;
+          for (unsigned k = 0; k < nth; ++k)
+            th.emplace_back([&, k] {
+              bool b0, c0;
+              gwa::newlineCount(t, len * k / nth, len * (k + 1) / nth, &cnt[k], &b0, &c0);
+              bl[k] = b0;
+              cr[k] = c0;
+            });
+          for (auto &x : th) x.join();
+          bool clean = len > 0 && t[0] != '\n';
+          uint64_t tot = 0;
+          std::vector<uint64_t> g0(nth);
+          for (unsigned k = 0; k < nth; ++k) {
+            clean = clean && !bl[k] && !cr[k];
+            g0[k] = tot;
+            tot += cnt[k];
+          }
+          if (clean) {
+            fast = true;
+            nrec = tot / 4;
+            starts.resize(nrec + 1);
+            starts[0] = 0;
+            th.clear();
+            for (unsigned k = 0; k < nth; ++k)
+              th.emplace_back([&, k] {
+                gwa::recordStartsFromNewlines(t, len * k / nth, len * (k + 1) / nth, g0[k], starts.data(), nrec + 1);
+              });
+            for (auto &x : th) x.join();
+            done = starts[nrec];  // the start of the first incomplete record
+            starts.resize(nrec);
+          }
+        }
+        if (!fast) done = gwa::frameRecords(t, len, fmt, final, ~0ull, &nrec, fmt == 1 ? &starts : nullptr);
+        frameS += secs(f0, Clock::now());
+        // batches of batchReads records; the records after the last full batch carry over
+        const uint64_t B = p->batchReads;
+        const uint64_t full = final ? (nrec + B - 1) / B : nrec / B;
+        uint64_t pos = 0;
+        if (fmt == 1) {
+          for (uint64_t k = 0; k < full && ok; ++k) {
+            const uint64_t r0i = k * B, r1i = std::min(nrec, r0i + B);
             Job j;
             j.id = id++;
             j.text = buf;
-            j.tb = pos;
-            j.te = e;
+            j.tb = base + starts[r0i];
+            j.te = base + (r1i < nrec ? starts[r1i] : done);
             j.format = fmt;
-            if (!run.push(std::move(j))) return;
-            nJobs = id;
-            pos = e;
+            j.starts.assign(starts.begin() + (long)r0i, starts.begin() + (long)r1i);
+            const uint64_t s0 = starts[r0i];
+            for (auto &x : j.starts) x -= s0;
+            if (!run.push(std::move(j))) ok = false;
           }
-          carry.assign(buf->data() + pos, buf->size() - pos);
-          if (final) break;
+          pos = (full * B < nrec) ? starts[full * B] : done;
+        } else {  // FASTA: frame again batch by batch (record starts are not kept)
+          uint64_t left = full == 0 ? 0 : nrec;
+          while (left > 0 && ok) {
+            uint64_t nr = 0;
+            const uint64_t e = pos + gwa::frameRecords(t + pos, len - pos, fmt, final, std::min<uint64_t>(B, left), &nr, nullptr);
+            if (nr == 0) break;
+            if (nr < B && !final) break;
+            Job j;
+            j.id = id++;
+            j.text = buf;
+            j.tb = base + pos;
+            j.te = base + e;
+            j.format = fmt;
+            if (!run.push(std::move(j))) ok = false;
+            pos = e;
+            left -= nr;
+          }
         }
-      } catch (std::exception &e) {
-        readErr = e.what();
-        run.fail(e.what());
+        if (!ok || final) break;
+        prev = buf;
+        carryFrom = base + pos;
+        carryLen = len - pos;
       }
-      readerDone = true;
-      run.finishJobs();
-      std::lock_guard<std::mutex> g(run.mu);
-      run.cv.notify_all();
-    });
-    // write batch results in order as they complete
-    uint64_t next = 0, n = 0;
-    bool ok = true;
-    for (;;) {
+    } catch (...) {
       {
-        std::unique_lock<std::mutex> g(run.mu);
-        run.cv.wait(g, [&] { return run.failed || run.done.count(next) != 0 || (readerDone && next >= nJobs); });
-        if (run.failed) { ok = false; break; }
-        if (run.done.count(next) == 0) break;  // reader finished and every batch was written
+        std::lock_guard<std::mutex> g(qmu);
+        stop = true;
+        qcv.notify_all();
       }
-      Result r;
-      if (!run.take(next, &r)) { ok = false; break; }
-      try {
-        writeAll(fd, r.r.sam, r.r.sam_len);
-      } catch (std::exception &e) {
-        gwa_results_free(&r.r);
-        run.fail(e.what());
-        ok = false;
-        break;
-      }
-      n += r.n;
-      gwa_results_free(&r.r);
-      ++next;
+      io.join();
+      throw;
     }
-    reader.join();
-    run.join();
-    gzclose(f);
-    if (!ok) throw std::runtime_error(run.err);
+    {
+      std::lock_guard<std::mutex> g(qmu);
+      stop = true;
+      qcv.notify_all();
+    }
+    io.join();
+    q.clear();
+    if (in >= 0) ::close(in);
+    in = -1;
+    run.finishJobs();
+    for (auto &t : run.workers) t.join();
+    run.workers.clear();
+    if (f) gzclose(f);
+    f = nullptr;
+    if (run.failed) throw std::runtime_error(run.err);
+    if (run.seekable) ::lseek(fd, (off_t)(run.base + run.nextOff), SEEK_SET);
+    const uint64_t n = run.fileReads;
     if (n_reads) *n_reads = n;
-    p->stats.reads = n;
-    p->stats.batches = next;
-    p->stats.wall_s = secs(t0, Clock::now());
-    p->stats.read_s = readS;
-    for (size_t d = 0; d < p->ix.size() && d < 16; ++d) p->stats.device_kernel_s[d] = run.devBusy[d];
+    gwa_pipeline_stats_t &st = p->stats;
+    st = gwa_pipeline_stats_t{};
+    st.reads = n;
+    st.batches = run.fileBatches;
+    st.wall_s = secs(t0, Clock::now());
+    st.read_s = readS;
+    st.frame_s = frameS;
+    for (size_t d = 0; d < p->ix.size() && d < 16; ++d) st.device_kernel_s[d] = run.devBusy[d];
+    st.parse_s = run.parseS;
+    st.setup_s = run.setupS;
+    st.format_s = run.formatS;
+    st.write_s = run.writeS;
+    st.order_wait_s = run.waitS;
     return 0;
   } catch (std::exception &e) {
     run.fail(e.what());
     run.join();
+    if (f) gzclose(f);
+    if (in >= 0) ::close(in);
     return gwa_fail_message(e.what());
   }
 }

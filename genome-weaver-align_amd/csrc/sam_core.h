@@ -11,13 +11,14 @@
 
 namespace gwa {
 
-// Read text and contig names as the formatter reads them (device or host memory).  Offsets are
-// relative to the blob starts.
+// Read text and contig names as the formatter reads them (device or host memory).  Read r's name
+// is name[nameB[r], nameE[r]) and its quality qual[qualB[r], qualE[r]): SoA blobs (nameE = nameB + 1)
+// or the fields of FASTQ records inside the file text itself.
 struct SamText {
   const char *name;
-  const uint64_t *nameOff;   // n + 1
+  const uint64_t *nameB, *nameE;
   const char *qual;          // nullptr: no qualities (SAM "*", as for FASTA input)
-  const uint64_t *qualOff;   // n + 1
+  const uint64_t *qualB, *qualE;
   const uint8_t *codes;      // ReadsView: the read as codes 0..4 (spaces skipped)
   const uint32_t *codeOff, *codeLen;
   const char *ctg;           // contig names
@@ -181,7 +182,7 @@ GWA_HD bool lineOne(SamOut &o, Ctx &cx, const Rec &r, const Rec *split, bool has
   if (eachMapped) flag |= 0x2;
   if (r.numBestHits <= 0) flag |= 0x4;
   if (split && split->numBestHits <= 0) flag |= 0x8;
-  o.bytes(cx.t.name + cx.t.nameOff[cx.r], cx.t.nameOff[cx.r + 1] - cx.t.nameOff[cx.r]);
+  o.bytes(cx.t.name + cx.t.nameB[cx.r], cx.t.nameE[cx.r] - cx.t.nameB[cx.r]);
   o.ch('\t');
   o.num(flag);
   o.ch('\t');
@@ -240,8 +241,8 @@ GWA_HD int samChain(SamOut &o, const SamText &t, uint32_t r, const OutHit *hits,
   const OutHit &h = hits[head];
   Ctx cx{t, r, hits, (int)t.codeLen[r], h.strand != 0 ? 1 : 0, t.qual == nullptr, 0, 0};
   if (!cx.qualNull) {
-    cx.q0 = t.qualOff[r];
-    cx.qn = t.qualOff[r + 1] - t.qualOff[r];
+    cx.q0 = t.qualB[r];
+    cx.qn = t.qualE[r] - t.qualB[r];
   }
   const int m = cx.m;
   const int fullQual = cx.qualNull ? 0 : (int)cx.qn;
@@ -320,12 +321,12 @@ GWA_HD int samChain(SamOut &o, const SamText &t, uint32_t r, const OutHit *hits,
 // The unmapped record: ReadHit("*", 0, 0, 0, 0, -1, FORWARD, CIGAR(), 0)
 // (S/BidirectionalSuffixFilter.java:258-261)
 GWA_HD void samUnmapped(SamOut &o, const SamText &t, uint32_t r) {
-  o.bytes(t.name + t.nameOff[r], t.nameOff[r + 1] - t.nameOff[r]);
+  o.bytes(t.name + t.nameB[r], t.nameE[r] - t.nameB[r]);
   o.lit("\t68\t*\t0\t1\t\t*\t0\t0\t");
   const uint8_t *c = t.codes + t.codeOff[r];
   for (uint32_t j = 0; j < t.codeLen[r]; ++j) o.ch(samfmt::kSym[c[j] > 4 ? 4 : c[j]]);
   o.ch('\t');
-  if (t.qual) o.bytes(t.qual + t.qualOff[r], t.qualOff[r + 1] - t.qualOff[r]);
+  if (t.qual) o.bytes(t.qual + t.qualB[r], t.qualE[r] - t.qualB[r]);
   else o.ch('*');
   o.ch('\n');
 }

@@ -52,7 +52,9 @@ class BatchStats(ctypes.Structure):
 
 class PipelineStats(ctypes.Structure):
     _fields_ = [("reads", ctypes.c_uint64), ("batches", ctypes.c_uint64), ("wall_s", ctypes.c_double),
-                ("read_s", ctypes.c_double), ("device_kernel_s", ctypes.c_double * 16)]
+                ("read_s", ctypes.c_double), ("device_kernel_s", ctypes.c_double * 16), ("parse_s", ctypes.c_double),
+                ("setup_s", ctypes.c_double), ("format_s", ctypes.c_double), ("write_s", ctypes.c_double),
+                ("order_wait_s", ctypes.c_double), ("frame_s", ctypes.c_double)]
 
 
 _lib = None

@@ -199,6 +199,13 @@ def align(ns, out=sys.stdout):
                         fd = None
                     if fd is not None:
                         n = pipe.align_file(ns.readFiles[0], fd)
+                        if ns.timing:
+                            st = pipe.stats()
+                            print("[gwa] pipeline %.2fs: read %.2fs, frame %.2fs; summed over %d worker threads: parse %.2fs, "
+                                  "set-up %.2fs, kernels %s s, SAM format %.2fs, write %.2fs, order wait %.2fs"
+                                  % (st.wall_s, st.read_s, st.frame_s, ns.workers * len(devices), st.parse_s, st.setup_s,
+                                     "/".join("%.2f" % st.device_kernel_s[i] for i in range(len(devices))),
+                                     st.format_s, st.write_s, st.order_wait_s), file=sys.stderr)
                     else:  # an in-memory stream (tests): through a temporary file
                         with tempfile.TemporaryFile() as tf:
                             n = pipe.align_file(ns.readFiles[0], tf.fileno())
@@ -206,10 +213,10 @@ def align(ns, out=sys.stdout):
                             out.write(tf.read().decode())
             finally:
                 pipe.close()
+        t2 = time.perf_counter()
     finally:
         for fm in fms:
             fm.close()
-    t2 = time.perf_counter()
     if ns.timing:
         print("[gwa] index load %.2fs (%d device(s)); align (read file -> SAM, index load excluded) %.2fs: %.0f reads/s"
               % (t1 - t0, len(devices), t2 - t1, n / max(t2 - t1, 1e-9)), file=sys.stderr)

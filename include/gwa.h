@@ -154,6 +154,10 @@ typedef struct {
   double wall_s;               /* the last align / align_file call */
   double read_s;               /* of which reading (and decompressing) the read file */
   double device_kernel_s[16];  /* per handle: time inside gwa_batch_run */
+  /* align_file stage times, summed over worker threads: read parse, batch set-up (H2D + encode),
+   * SAM formatting + D2H, output writes, and waiting for the batch-order output position */
+  double parse_s, setup_s, format_s, write_s, order_wait_s;
+  double frame_s;  /* reader thread: framing the text into batches of complete records */
 } gwa_pipeline_stats_t;
 int gwa_pipeline_open(gwa_index_t *const *ix, int n_ix, const gwa_config_t *cfg, uint32_t batch_reads,
                       int workers_per_device, gwa_pipeline_t **out);

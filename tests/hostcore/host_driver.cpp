@@ -94,8 +94,8 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
     const char *qv = quals ? quals[i] : nullptr;
     const uint64_t nameOff[2] = {0, strlen(names[i])}, qualOff[2] = {0, qv ? strlen(qv) : 0};
     const uint32_t codeOff[1] = {0}, codeLen[1] = {(uint32_t)mlen};
-    const SamText t{names[i], nameOff, qv, qualOff, codes.data(), codeOff, codeLen, sn.blob.data(), sn.off.data(),
-                    rk.data(), sn.starKey, sn.emptyKey};
+    const SamText t{names[i], nameOff, nameOff + 1, qv, qualOff, qualOff + 1, codes.data(), codeOff, codeLen,
+                    sn.blob.data(), sn.off.data(), rk.data(), sn.starKey, sn.emptyKey};
     if (hd.status == ST_MAPPED || hd.status == ST_UNMAPPED) {
       SamOut cnt{nullptr, 0};
       if (samRead(cnt, t, 0, hd, oh.data(), oc.data()) != 0) return -2;

@@ -196,3 +196,41 @@ def test_bd_bwa_print_the_header_only(tmp_path, m):
     ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-m", m, str(rp)])
     assert gwa_cli.align(ns, out=out) == len(reads)
     assert out.getvalue() == O.Index.from_fasta(ref.read_text()).sam_header()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(len(FASTQ_CASES)))
+def test_cli_device_fastq_parse_edge_cases(tmp_path, i):
+    # the pipeline locates FASTQ fields on the GPU (batch_io.hip fastqFieldsKernel): CRLF / CR line
+    # ends, blank lines between records, odd header whitespace, empty reads and a missing final newline
+    # give the records the host parser (and gwa_cli.read_fastq) gives
+    import oracle as O
+    import synth
+    codes, names, lengths = synth.genome([("chrA", 30000)], config_id=14)
+    ref = tmp_path / "ref.fa"
+    ref.write_text(synth.fasta_text(codes, names, lengths))
+    s = synth.to_strings(synth.reads(codes, lengths, 40, 60, 1, config_id=15)[0])
+    body = b"".join(b"@r%d desc\r\n%s\r\n+\r\n%s\r\n%s" % (k, s[k].encode(), b"I" * 60, b"\n" if k % 3 == 0 else b"")
+                    for k in range(40))
+    text = FASTQ_CASES[i] + b"\n" + body
+    rp = tmp_path / "reads.fq"
+    rp.write_bytes(text)
+    recs = _py_records(text, "fastq")
+    out = io.StringIO()
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-k", "1", "--batch", "7", str(rp)])
+    assert gwa_cli.align(ns, out=out) == len(recs)
+    oi = O.Index.from_fasta(ref.read_text())
+    assert out.getvalue() == oi.sam_header() + oi.align(recs, O.OrcConfig.default(k=1.0))
+
+
+@pytest.mark.gpu
+def test_cli_malformed_fastq_reports_the_record(tmp_path):
+    import synth
+    codes, names, lengths = synth.genome([("chrA", 30000)], config_id=14)
+    ref = tmp_path / "ref.fa"
+    ref.write_text(synth.fasta_text(codes, names, lengths))
+    rp = tmp_path / "bad.fq"
+    rp.write_bytes(b"@a\nACGT\n+\nIIII\n@b\nACGT\n+\nIII\n")
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), str(rp)])
+    with pytest.raises(gwa.GwaError, match="malformed FASTQ record"):
+        gwa_cli.align(ns, out=io.StringIO())
