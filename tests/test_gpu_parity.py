@@ -311,3 +311,42 @@ def test_per_read_counters_match_oracle_stats(random_pair):
     assert np.array_equal(c[:, 1], fm), np.nonzero(c[:, 1] != fm)[0][:5]
     assert np.array_equal(c[:, 2], qs), np.nonzero(c[:, 2] != qs)[0][:5]
     assert np.array_equal(c[:, 16], sw), np.nonzero(c[:, 16] != sw)[0][:5]
+
+
+# ---- hg19-like repetitive genome (tools/synth.genome_repeats): N gaps, repeat families, satellites,
+# segmental duplications at 0.5 % of hg19 size ----
+
+@pytest.fixture(scope="module")
+def hg19r_pair():
+    import gwa
+    codes, names, lengths = synth.genome_repeats(synth.HG19_CONTIGS, config_id=1, scale=0.005)
+    gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths)
+    # the oracle index takes the GPU suffix arrays after an independent check of them (permutation +
+    # 2^17 sampled adjacent pairs per strand; pairs inside segmental duplications compare ~100 kb)
+    sa_f, sa_r = gi.suffixArray(0), gi.suffixArray(1)
+    O.check_cyclic_sa(codes, sa_f, samples=1 << 17)
+    O.check_cyclic_sa(np.ascontiguousarray(codes[::-1]), sa_r, samples=1 << 17)
+    oi = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
+    return codes, lengths, gi, oi
+
+
+@pytest.mark.parametrize("strategy", ["bsf", "sf"])
+def test_hg19r_c2_k2(hg19r_pair, strategy):
+    codes, lengths, gi, oi = hg19r_pair
+    strs = synth.to_strings(synth.reads_codes(codes, lengths, 4000, 100, 2, config_id=2))
+    sam = _check(gi, oi, [("r%d" % i, strs[i], "I" * 100) for i in range(len(strs))], k=2.0, strategy=strategy)
+    # repeats make multi-hit (X0 > 1) records common
+    assert sum(1 for l in sam.splitlines() if "\tX0:i:1" not in l) > 50
+
+
+@pytest.mark.parametrize("strategy", ["bsf", "sf"])
+def test_hg19r_c4_indels_k5(hg19r_pair, strategy):
+    codes, lengths, gi, oi = hg19r_pair
+    strs = synth.to_strings(synth.reads_codes(codes, lengths, 600, 150, 2, config_id=4, indels=True, max_edits=5))
+    _check(gi, oi, [("r%d" % i, strs[i], "I" * 150) for i in range(len(strs))], k=5.0, strategy=strategy)
+
+
+def test_hg19r_allhits(hg19r_pair):
+    codes, lengths, gi, oi = hg19r_pair
+    strs = synth.to_strings(synth.reads_codes(codes, lengths, 1500, 100, 2, config_id=6))
+    _check(gi, oi, [("r%d" % i, strs[i], "I" * 100) for i in range(len(strs))], k=2.0, reportType="allhits")
