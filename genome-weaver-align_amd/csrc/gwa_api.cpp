@@ -1046,6 +1046,8 @@ static void formatResults(gwa_batch *b, const uint32_t *hostIdx, uint32_t first,
   out->n_reads = n;
   out->sam = nullptr;
   out->line_off = nullptr;
+  out->records = nullptr;
+  out->n_records = 0;
   if (b->headerOnly) {
     if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
     out->sam = (char *)calloc(1, 1);
@@ -1172,8 +1174,105 @@ void gwa_results_free(gwa_results_t *r) {
   if (!r) return;
   free(r->sam);
   free(r->line_off);
+  free(r->records);
   r->sam = nullptr;
   r->line_off = nullptr;
+  r->records = nullptr;
+  r->n_records = 0;
+}
+
+int gwa_results_records(const gwa_index_t *ix, gwa_results_t *r) {
+  try {
+    free(r->records);
+    r->records = nullptr;
+    r->n_records = 0;
+    std::vector<gwa_record_t> recs;
+    const HostIndex &h = ix->host;
+    // contig name -> index (the first contig of that name, as String.equals lookups would find)
+    std::vector<std::pair<std::string, int>> byName;
+    for (size_t i = 0; i < h.names.size(); ++i) byName.push_back({h.names[i], (int)i});
+    std::stable_sort(byName.begin(), byName.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    auto refOf = [&](const char *p, size_t n) -> int {
+      if (n == 1 && p[0] == '*') return -1;
+      const std::string k(p, n);
+      auto it = std::lower_bound(byName.begin(), byName.end(), k, [](const auto &a, const std::string &x) { return a.first < x; });
+      if (it == byName.end() || it->first != k) throw std::runtime_error("SAM record names an unknown contig: " + k);
+      return it->second;
+    };
+    const char *t = r->sam;
+    for (uint32_t i = 0; i < r->n_reads; ++i) {
+      uint64_t a = r->line_off[i];
+      const uint64_t e = r->line_off[i + 1];
+      while (a < e) {
+        const char *nl = (const char *)memchr(t + a, '\n', e - a);
+        const uint64_t le = nl ? (uint64_t)(nl - t) : e;
+        // the tab-separated fields of the line
+        std::vector<std::pair<uint64_t, uint64_t>> f;
+        uint64_t b = a;
+        for (uint64_t x = a; x <= le; ++x)
+          if (x == le || t[x] == '\t') {
+            f.push_back({b, x - b});
+            b = x + 1;
+          }
+        if (f.size() < 11) throw std::runtime_error("malformed SAM line in results");
+        gwa_record_t g{};
+        g.read = i;
+        g.flag = (uint32_t)strtoul(std::string(t + f[1].first, f[1].second).c_str(), nullptr, 10);
+        g.ref = refOf(t + f[2].first, f[2].second);
+        g.pos = (int32_t)strtol(std::string(t + f[3].first, f[3].second).c_str(), nullptr, 10);
+        g.end = g.pos;
+        g.strand = (g.flag & 0x10) ? 1 : 0;
+        g.nm = -1;
+        g.x0 = 0;
+        g.split = -1;
+        g.line_off = a; g.line_len = (uint32_t)(le - a);
+        g.name_off = f[0].first; g.name_len = (uint32_t)f[0].second;
+        g.cigar_off = f[5].first; g.cigar_len = (uint32_t)f[5].second;
+        g.seq_off = f[9].first; g.seq_len = (uint32_t)f[9].second;
+        g.qual_off = f[10].first; g.qual_len = (uint32_t)f[10].second;
+        g.qual_null = (f[10].second == 1 && t[f[10].first] == '*') ? 1 : 0;
+        for (size_t k = 11; k < f.size(); ++k) {
+          const char *p = t + f[k].first;
+          if (f[k].second >= 5 && !memcmp(p, "NM:i:", 5)) g.nm = (int32_t)strtol(std::string(p + 5, f[k].second - 5).c_str(), nullptr, 10);
+          else if (f[k].second >= 5 && !memcmp(p, "X0:i:", 5)) g.x0 = (int32_t)strtol(std::string(p + 5, f[k].second - 5).c_str(), nullptr, 10);
+          else if (f[k].second >= 5 && !memcmp(p, "XP:Z:", 5)) { g.state_off = f[k].first + 5; g.state_len = (uint32_t)(f[k].second - 5); }
+        }
+        // a first line with FLAG 0x1 and without 0x80 is followed by its split record
+        if (!recs.empty() && recs.back().split == -2) {
+          gwa_record_t &first = recs.back();
+          first.split = (int32_t)recs.size();
+          g.is_split = 1;
+        }
+        if ((g.flag & 0x1) && !(g.flag & 0x80) && !g.is_split) {
+          g.split = -2;  // (resolved by the next line)
+          g.end = g.pos;
+        }
+        recs.push_back(g);
+        a = le + 1;
+      }
+    }
+    // the split record's end = POS + TLEN of its first line (AlignmentRecord.toSAMLine prints
+    // split.end - start as TLEN)
+    for (size_t k = 0; k < recs.size(); ++k) {
+      if (recs[k].split == -2) throw std::runtime_error("SAM results end inside a split record pair");
+      if (recs[k].split >= 0) {
+        const gwa_record_t &g = recs[k];
+        const char *p = t + g.line_off;
+        // TLEN is field 9 (index 8)
+        int tab = 0;
+        uint64_t x = 0;
+        while (x < g.line_len && tab < 8) tab += p[x++] == '\t';
+        recs[(size_t)g.split].end = g.pos + (int32_t)strtol(p + x, nullptr, 10);
+      }
+    }
+    r->records = (gwa_record_t *)malloc(sizeof(gwa_record_t) * std::max<size_t>(1, recs.size()));
+    if (!r->records) throw std::runtime_error("out of host memory for the records");
+    if (!recs.empty()) memcpy(r->records, recs.data(), sizeof(gwa_record_t) * recs.size());
+    r->n_records = recs.size();
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
 }
 
 int gwa_align_batch(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_results_t *out) {

@@ -451,6 +451,8 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
     uint64_t total = 0;
     for (auto &r : parts) total += r.r.sam_len;
     out->n_reads = n;
+    out->records = nullptr;
+    out->n_records = 0;
     out->sam = (char *)malloc(total + 1);
     out->sam_len = total;
     out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n + 1));

@@ -35,9 +35,17 @@ class _ReadBuf(ctypes.Structure):
     _fields_ = [("reads", _Reads), ("priv", ctypes.c_void_p)]
 
 
+class Record(ctypes.Structure):
+    """gwa_record_t: one SAM record as AlignmentRecord fields (string fields index the SAM text)."""
+    _fields_ = [(n, ctypes.c_uint32) for n in ("read", "flag")] + [(n, ctypes.c_int32) for n in (
+        "ref", "pos", "end", "strand", "nm", "x0", "split", "is_split", "qual_null", "pad_")] + [
+        (n, ctypes.c_uint64) for n in ("line_off", "name_off", "cigar_off", "seq_off", "qual_off", "state_off")] + [
+        (n, ctypes.c_uint32) for n in ("line_len", "name_len", "cigar_len", "seq_len", "qual_len", "state_len")]
+
+
 class _Results(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_uint32), ("sam", ctypes.c_void_p), ("sam_len", ctypes.c_uint64),
-                ("line_off", ctypes.c_void_p)]
+                ("line_off", ctypes.c_void_p), ("records", ctypes.c_void_p), ("n_records", ctypes.c_uint64)]
 
 
 class BatchStats(ctypes.Structure):
@@ -64,7 +72,7 @@ EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_inde
            "gwa_index_build_codes", "gwa_index_save", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
            "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
            "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
-           "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_batch_results_select",
+           "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_results_records", "gwa_batch_results_select",
            "gwa_pipeline_open", "gwa_pipeline_align", "gwa_pipeline_align_file", "gwa_pipeline_stats",
            "gwa_pipeline_close", "gwa_reads_parse", "gwa_reads_free"]
 
@@ -91,6 +99,7 @@ def lib():
         L.gwa_index_close.argtypes = [V]
         L.gwa_align_batch.argtypes = [V, P(_Config), P(_Reads), P(_Results)]
         L.gwa_results_free.argtypes = [P(_Results)]
+        L.gwa_results_records.argtypes = [V, P(_Results)]
         L.gwa_free.argtypes = [V]
         L.gwa_batch_create.argtypes = [V, P(_Config), P(_Reads), P(V)]
         L.gwa_batch_run.argtypes = [V]
@@ -484,6 +493,20 @@ class Batch:
         res = _Results()
         _check(lib().gwa_batch_results_select(self.h, idx.ctypes.data, len(idx), ctypes.byref(res)))
         return _take_results(res)
+
+    def records(self, index, first=0, count=None):
+        """(SAM text, [Record]) of reads [first, first + count): the AlignmentRecord fields of every line
+        (include/gwa.h gwa_results_records)."""
+        res = _Results()
+        _check(lib().gwa_batch_results_range(self.h, first, self.n - first if count is None else count,
+                                             ctypes.byref(res)))
+        try:
+            _check(lib().gwa_results_records(index.h, ctypes.byref(res)))
+            recs = [Record.from_buffer_copy(ctypes.string_at(res.records + i * ctypes.sizeof(Record), ctypes.sizeof(Record)))
+                    for i in range(res.n_records)]
+            return (ctypes.string_at(res.sam, res.sam_len).decode() if res.sam_len else ""), recs
+        finally:
+            lib().gwa_results_free(ctypes.byref(res))
 
     def sam_size(self):
         """Format the whole batch's SAM text in the library (D2H of the records + host formatting) and

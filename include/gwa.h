@@ -54,13 +54,37 @@ typedef struct {
   void *priv;
 } gwa_read_buf_t;
 
+/* One SAM record as the fields of the reference's AlignmentRecord (R/AlignmentRecord.java:44-79:
+ * readName, chr, strand, start, end, numMismatches, cigar, querySeq, qual, score = 1, numBestHits,
+ * alignmentState, split), so a JVM binding can build the objects SAMOutput.emit prints
+ * (A/SAMOutput.java:73-82).  String fields are (offset, length) into gwa_results_t.sam. */
+typedef struct {
+  uint32_t read;          /* input index of the read */
+  uint32_t flag;          /* SAM FLAG */
+  int32_t ref;            /* contig index of chr; -1 = "*" */
+  int32_t pos;            /* start */
+  int32_t end;            /* end where the text fixes it (a split record: POS + TLEN of its first line), else pos */
+  int32_t strand;         /* 0 = Strand.FORWARD, 1 = REVERSE (FLAG 0x10) */
+  int32_t nm;             /* numMismatches: NM:i, -1 when the line has none */
+  int32_t x0;             /* numBestHits: X0:i, 0 when absent (unmapped) */
+  int32_t split;          /* index (in the record array) of this record's split record, -1 = none */
+  int32_t is_split;       /* 1: this record is another record's split (emit the first one only) */
+  int32_t qual_null;      /* 1: QUAL is "*" (qual == null) */
+  int32_t pad_;
+  uint64_t line_off, name_off, cigar_off, seq_off, qual_off, state_off;
+  uint32_t line_len, name_len, cigar_len, seq_len, qual_len, state_len;
+} gwa_record_t;
+
 /* Library-owned SAM text (no header), in input order; read i's lines are
- * sam[line_off[i], line_off[i+1]).  Free with gwa_results_free. */
+ * sam[line_off[i], line_off[i+1]).  Free with gwa_results_free.  records / n_records are filled on
+ * request by gwa_results_records (NULL / 0 until then). */
 typedef struct {
   uint32_t n_reads;
   char *sam;
   uint64_t sam_len;
   uint64_t *line_off; /* n_reads + 1 */
+  gwa_record_t *records;
+  uint64_t n_records;
 } gwa_results_t;
 
 /* Per-batch counters (instrumentation for SURVEY.md §8d roofline accounting). */
@@ -112,6 +136,8 @@ void gwa_index_close(gwa_index_t *ix);
 /* One call per batch: H2D, align on the GPU, D2H, SAM formatting. */
 int gwa_align_batch(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_results_t *out);
 void gwa_results_free(gwa_results_t *r);
+/* Fill r->records (one gwa_record_t per SAM line, in text order) from the SAM text of r. */
+int gwa_results_records(const gwa_index_t *ix, gwa_results_t *r);
 void gwa_free(void *p);
 
 /* Parse the complete records of text[0, len): format 0 = FASTA, 1 = FASTQ.  With final = 0 the

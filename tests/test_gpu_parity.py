@@ -350,3 +350,62 @@ def test_hg19r_allhits(hg19r_pair):
     codes, lengths, gi, oi = hg19r_pair
     strs = synth.to_strings(synth.reads_codes(codes, lengths, 1500, 100, 2, config_id=6))
     _check(gi, oi, [("r%d" % i, strs[i], "I" * 100) for i in range(len(strs))], k=2.0, reportType="allhits")
+
+
+def _to_sam_line(text, names, r, split=None, has_segments=None, is_first=True, each_mapped=True):
+    """AlignmentRecord.toSAMLine (R/AlignmentRecord.java:109-170) from gwa_record_t fields -- what a
+    JVM binding does with the objects it builds from the records."""
+    s = lambda off, n: text[off:off + n]
+    if has_segments is None:
+        has_segments = split is not None
+    flag = 0x1 if has_segments else 0
+    if r.strand == 1:
+        flag |= 0x10
+    if is_first:
+        flag |= 0x40
+        if r.x0 <= 0 or (split is not None and split.x0 <= 0):
+            each_mapped = False
+    elif split is None:
+        flag |= 0x80
+    if each_mapped:
+        flag |= 0x2
+    if r.x0 <= 0:
+        flag |= 0x4
+    if split is not None and split.x0 <= 0:
+        flag |= 0x8
+    chr_ = "*" if r.ref < 0 else names[r.ref]
+    cols = [s(r.name_off, r.name_len), str(flag), chr_, str(r.pos), "1", s(r.cigar_off, r.cigar_len)]
+    if split is None:
+        cols += ["*", "0", "0"]
+    else:
+        sc = "*" if split.ref < 0 else names[split.ref]
+        cols += ["=" if chr_ != "*" and chr_ == sc else sc, str(split.pos), str(split.end - r.pos)]
+    cols += [s(r.seq_off, r.seq_len), "*" if r.qual_null else s(r.qual_off, r.qual_len)]
+    if r.x0 > 0:
+        if r.nm >= 0:
+            cols.append("NM:i:%d" % r.nm)
+        cols += ["XP:Z:" + s(r.state_off, r.state_len), "X0:i:%d" % r.x0]
+    line = "\t".join(cols)
+    if split is not None:
+        line += "\n" + _to_sam_line(text, names, split, None, has_segments, False, each_mapped)
+    return line
+
+
+def test_results_records_rebuild_the_sam(repetitive_pair):
+    # gwa_results_records: the AlignmentRecord fields of every line; rebuilding each top-level record
+    # with toSAMLine gives the SAM text back (chimeric reads -> split records, unmapped reads)
+    import gwa
+    from test_hostcore import _mk
+    codes, gi, oi = repetitive_pair
+    rng = np.random.default_rng(72)
+    reads = _mk(codes, 400, 100, 3, True, seed=71) + [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), "I" * 100)
+                                                       for i in range(20)]
+    b = gwa.Batch(gi, gwa.AlignmentConfig(k=0.1), reads)
+    b.run()
+    sam, recs = b.records(gi)
+    b.close()
+    names = ["chrA", "chrB", "chr10"]
+    assert len(recs) == len(sam.splitlines())
+    assert any(r.split >= 0 for r in recs) and any(r.ref < 0 for r in recs)
+    rebuilt = [_to_sam_line(sam, names, r, recs[r.split] if r.split >= 0 else None) for r in recs if not r.is_split]
+    assert "\n".join(rebuilt) + "\n" == sam
