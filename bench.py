@@ -95,8 +95,9 @@ def main():
                          "repeats and N gaps (tools/synth.genome_repeats); ecoli; or a size in Mbp")
     ap.add_argument("--reads", type=int, default=int(os.environ.get("GWA_BENCH_READS", "0")))
     ap.add_argument("--k", type=float, default=None, help="max edits (default: 2 for c2, 5 for c4)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4"],
-                    help="c2: 100 bp, 0-2 substitutions (the BASELINE metric); c4: 150 bp, 0-5 edits with indels")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
+                    help="c2: 100 bp, 0-2 substitutions (the BASELINE metric); c4: 150 bp, 0-5 edits with indels; "
+                         "c5: 2x100 bp paired-end, insert ~ N(300, 30), proper pairs within [210, 390]")
     ap.add_argument("--strategy", default="bsf", choices=["bsf", "sf"], help="-m (align strategy)")
     ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "100000")),
                     help="reads of the single-thread CPU baseline (SURVEY.md 8(d)(i))")
@@ -160,6 +161,8 @@ def main():
     log("index built + resident in HBM: %.1fs, %.2f GB" % (t_index, gi.deviceBytes() / 1e9))
 
     cfg = gwa.AlignmentConfig(k=args.k, strategy=args.strategy)
+    if args.workload == "c5":
+        return bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_index)
     # synthetic reads: C2 100 bp with 0-2 substitutions; C4 150 bp with 0-5 edits,
     # 60 % substitutions / 20 % 1-bp insertions / 20 % 1-bp deletions; shard = rank
     m = 150 if c4 else 100
@@ -386,6 +389,131 @@ def main():
                    "mapped": st.n_mapped, "unmapped": st.n_unmapped, "index_build_s": t_index,
                    "index_gb": gi.deviceBytes() / 1e9, "parity": parity},
     }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    batch.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_index):
+    """Config C5: 2x100 bp pairs (tools/synth.pairs_codes: insert ~ N(300, 30)), -k 2.  One step = the
+    alignment kernels over both mates of every pair plus the pairing and SAM text written in HBM
+    (gwa_batch_format), reads resident in HBM.  value = reads/s (two per pair).  The pairing rules are
+    the build's own (the reference has no paired-end path); parity is against the oracle's
+    restatement of them (orc_align_pairs)."""
+    import numpy as np
+    import synth
+    import gwa
+    import dist as gdist
+    import torch
+    if dist:
+        import torch.distributed as tdist
+    m = 100
+    pairs = (args.reads or 10_000_000) // 2
+    t0 = time.time()
+    m1, m2 = synth.pairs_codes(codes, lengths, pairs, m, config_id=5, shard=rank)
+    s1, s2 = synth.SYM[m1].tobytes(), synth.SYM[m2].tobytes()
+    del m1, m2
+    off = np.arange(0, m * (pairs + 1), m, dtype=np.uint64)
+    nb, no = synth.name_blob(pairs)
+    q1, q2 = b"I" * (m * pairs), b"J" * (m * pairs)
+    log("pairs generated in %.1fs" % (time.time() - t0))
+    cfg = gwa.AlignmentConfig(k=args.k, strategy="bsf")
+    batch = gwa.Batch(gi, cfg, pair_blobs=((nb, no, s1, off, q1, off), (nb, no, s2, off, q2, off)))
+
+    def pair_tuple(i):
+        n = nb[10 * i:10 * i + 10].decode()
+        return (n, s1[m * i:m * i + m].decode(), "I" * m), (n, s2[m * i:m * i + m].decode(), "J" * m)
+
+    for _ in range(args.warmup):
+        batch.run()
+        batch.format_device()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = qms = sms = 0.0
+    for _ in range(args.steps):
+        batch.run()
+        st = batch.stats()
+        kms += st.kernel_ms
+        qms += st.quickscan_ms
+        sms += st.search_ms
+        batch.format_device()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    rank_times = gdist.all_gather_floats(time.perf_counter() - t0)
+    dt = max(rank_times)
+    value = 2 * pairs * args.steps * world / dt
+    st = batch.stats()
+    parity = cpu = cpu1 = None
+    if rank == 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        T, tdesc = host_cores()
+        sa_f, sa_r = gi.suffixArray(0), gi.suffixArray(1)
+        O.check_cyclic_sa(codes, sa_f, samples=args.sa_check, seed=11, threads=T)
+        O.check_cyclic_sa(np.ascontiguousarray(codes[::-1]), sa_r, samples=args.sa_check, seed=12, threads=T)
+        oi = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
+        del sa_f, sa_r
+        ocfg = O.OrcConfig.default(k=args.k)
+        if args.check:
+            samp = np.sort(np.random.default_rng(7).choice(pairs, min(args.check, pairs), replace=False)).astype(np.uint32)
+            got, _ = batch.results_select(samp)
+            tp = [pair_tuple(int(i)) for i in samp]
+            exp = oi.align_pairs([a for a, b in tp], [b for a, b in tp], ocfg)
+            parity = {"pairs": int(len(samp)), "identical": got == exp,
+                      "note": "random pairs vs the oracle's restatement of the build's pairing rules (parity unpinned "
+                              "against the reference, which has no paired-end path)"}
+            log("parity on %d pairs: %s" % (len(samp), got == exp))
+        if not args.no_cpu:
+            from concurrent.futures import ThreadPoolExecutor
+            model = cpu_model()
+            ns = min(args.cpu_sample // 2, pairs)
+            tp = [pair_tuple(i) for i in range(ns)]
+            t1 = time.perf_counter()
+            oi.align_pairs([a for a, b in tp], [b for a, b in tp], ocfg)
+            ct = time.perf_counter() - t1
+            cpu1 = {"value": 2 * ns / ct, "unit": "reads/s", "cores": 1, "kind": "port", "seconds": ct,
+                    "sample": "first %d pairs, single-thread C++ oracle (paired-end restatement of the build's rules over "
+                              "the reference BSF path; CPU restatement, not the JVM); %s" % (ns, model)}
+            cpu = cpu1
+            if T > 1:
+                npairs = int(min(pairs, max(ns, args.cpu_seconds * cpu1["value"] / 2 * T)))
+                tp = tp + [pair_tuple(i) for i in range(ns, npairs)]
+                chunks = [(a * npairs // T, (a + 1) * npairs // T) for a in range(T)]
+                t1 = time.perf_counter()
+                with ThreadPoolExecutor(T) as ex:
+                    list(ex.map(lambda c: oi.align_pairs([x for x, y in tp[c[0]:c[1]]], [y for x, y in tp[c[0]:c[1]]],
+                                                         ocfg), chunks))
+                ct = time.perf_counter() - t1
+                cpu = {"value": 2 * npairs / ct, "unit": "reads/s", "cores": T, "kind": "port", "seconds": ct,
+                       "sample": "first %d pairs on %d host threads (%s; contiguous ranges), C++ oracle; %s"
+                                 % (npairs, T, tdesc, model)}
+            log("cpu baseline: %.0f reads/s (%d threads)" % (cpu["value"], cpu["cores"]))
+    steps = args.steps
+    q_ms, s_ms = qms / steps, sms / steps
+    q_ref = 64.0 * (st.quick_blocks + st.quick_short_steps) + 4.0 * st.quick_sa_reads
+    s_ref = (64.0 * (st.blocks - st.quick_blocks + st.search_short_steps) + 4.0 * (st.sa_reads - st.quick_sa_reads)
+             + st.verify_bytes)
+    dom, dom_ref, dom_ms = ("fm_quickscan", q_ref, q_ms) if q_ms >= s_ms else ("bsf_search", s_ref, s_ms)
+    ach = dom_ref / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    out = {"metric": "reads/sec, 2x100 bp paired-end k<=2 vs hg19 (config C5)", "value": value, "unit": "reads/s",
+           "n_gpus": world, "steps": steps, "warmup": args.warmup, "ms_per_step": dt * 1e3 / steps,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": "%s; %d pairs (2 x 100 bp, insert ~ N(300, 30), 0-2 substitutions per mate) per GPU "
+                                  "per step, -k %g, -m bsf, proper pairs in [210, 390]" % (gname, pairs, args.k),
+                      "genome_bp": int(len(codes)), "pairs_per_gpu_per_step": pairs,
+                      "parallelism": "pairs sharded, index replicated (%d GPU)" % world},
+           "roofline": {"bound": "hbm", "kernel": dom, "definition": "SURVEY.md 8(d) algorithmic bytes",
+                        "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                        "traffic": None, "algorithmic_bytes_per_launch": dom_ref, "avg_launch_ms": dom_ms},
+           "cpu_baseline": cpu,
+           "detail": {"rank_seconds": rank_times, "quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
+                      "tier_reads": list(st.tier_reads), "tier_ms": [round(x, 3) for x in st.tier_ms],
+                      "cpu_baseline_1thread": cpu1, "parity": parity, "index_build_s": t_index}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     batch.close()

@@ -152,10 +152,17 @@ void launchFastqFields(const char *text, uint64_t len, const uint64_t *start, ui
 
 // ---- SAM out ----
 
+// one read's records, or (pairs mode, ps.np > 0) pair r's two mate lines
+__device__ __forceinline__ int samUnit(SamOut &o, const SamText &t, uint32_t r, const OutHeader *oh, const OutHit *hits,
+                                       const uint16_t *cig, const PairSpec &ps) {
+  if (ps.np) return samPair(o, t, r, ps.np, oh, hits, cig, ps.minIns, ps.maxIns);
+  return samRead(o, t, r, oh[r], hits, cig);
+}
+
 __global__ void __launch_bounds__(256) samLenKernel(SamText t, const OutHeader *__restrict__ oh, const OutHit *__restrict__ hits,
                                                     const uint16_t *__restrict__ cig, const uint32_t *__restrict__ idx,
                                                     uint32_t first, uint32_t n, uint64_t *__restrict__ len,
-                                                    uint32_t *__restrict__ err) {
+                                                    uint32_t *__restrict__ err, PairSpec ps) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j > n) return;
   if (j == n) {  // the scan's total
@@ -164,7 +171,7 @@ __global__ void __launch_bounds__(256) samLenKernel(SamText t, const OutHeader *
   }
   const uint32_t r = idx ? idx[j] : first + j;
   SamOut o{nullptr, 0};
-  if (samRead(o, t, r, oh[r], hits, cig) != 0) {
+  if (samUnit(o, t, r, oh, hits, cig, ps) != 0) {
     atomicMin(err, j);
     o.n = 0;
   }
@@ -174,25 +181,25 @@ __global__ void __launch_bounds__(256) samLenKernel(SamText t, const OutHeader *
 __global__ void __launch_bounds__(256) samWriteKernel(SamText t, const OutHeader *__restrict__ oh, const OutHit *__restrict__ hits,
                                                       const uint16_t *__restrict__ cig, const uint32_t *__restrict__ idx,
                                                       uint32_t first, uint32_t n, const uint64_t *__restrict__ off,
-                                                      char *__restrict__ out) {
+                                                      char *__restrict__ out, PairSpec ps) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t r = idx ? idx[j] : first + j;
   SamOut o{out + off[j], 0};
-  (void)samRead(o, t, r, oh[r], hits, cig);
+  (void)samUnit(o, t, r, oh, hits, cig, ps);
 }
 
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
                      uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
-                     uint32_t *err, char *out, int pass, hipStream_t s) {
+                     uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps) {
   const dim3 grid((n + 1 + 255) / 256);
   if (pass == 0) {
-    hipLaunchKernelGGL(samLenKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, len, err);
+    hipLaunchKernelGGL(samLenKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, len, err, ps);
     FCHK(hipGetLastError());
   } else if (pass == 1) {  // exclusive scan of n + 1 lengths: off[n] = total bytes
     FCHK(rocprim::exclusive_scan(scanTmp, *scanTmpBytes, len, off, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), s));
   } else {
-    hipLaunchKernelGGL(samWriteKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, off, out);
+    hipLaunchKernelGGL(samWriteKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
     FCHK(hipGetLastError());
   }
 }

@@ -127,6 +127,8 @@ struct gwa_batch {
   gwa_batch_stats_t stats{};
   bool ran = false;
   bool headerOnly = false;  // -m bd / -m bwa: the reference emits no SAM records (see gwa_batch_create)
+  uint32_t pairs = 0;       // paired-end batch: mate 1 of pair i = read i, mate 2 = read pairs + i
+  int32_t minIns = 0, maxIns = 0;
   std::vector<std::pair<uint32_t, int>> deep;  // (read, tier) of every read rerun on a tier >= 1
 };
 
@@ -1009,18 +1011,24 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
   }
   HIPCHK(hipMemsetAsync(b->d_fmtErr, 0xFF, sizeof(uint32_t), s));
   const SamText t = samText(b);
+  const PairSpec ps{b->pairs, b->minIns, b->maxIns};
   size_t tmpBytes = b->fmtTmpBytes;
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
-                  b->d_fmtErr, nullptr, 0, s);
+                  b->d_fmtErr, nullptr, 0, s, ps);
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
-                  b->d_fmtErr, nullptr, 1, s);
+                  b->d_fmtErr, nullptr, 1, s, ps);
   uint64_t total = 0;
   uint32_t err = 0;
   HIPCHK(hipMemcpyAsync(&total, b->d_fmtOff + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&err, b->d_fmtErr, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (err != 0xFFFFFFFFu) {  // a read the reference would abort on, or whose search failed
-    const uint32_t r = hostIdx ? hostIdx[err] : first + err;
+    uint32_t r = hostIdx ? hostIdx[err] : first + err;
+    if (b->pairs) {  // the failing mate of pair r
+      OutHeader h1;
+      HIPCHK(hipMemcpy(&h1, b->d_oh + r, sizeof(h1), hipMemcpyDeviceToHost));
+      if (h1.status == ST_MAPPED || h1.status == ST_UNMAPPED) r += b->pairs;
+    }
     OutHeader h;
     uint64_t no[2];
     HIPCHK(hipMemcpy(&h, b->d_oh + r, sizeof(h), hipMemcpyDeviceToHost));
@@ -1036,7 +1044,7 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
   }
   growDev(&b->d_fmtText, &b->fmtTextCap, (size_t)total + 1);
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
-                  b->d_fmtErr, b->d_fmtText, 2, s);
+                  b->d_fmtErr, b->d_fmtText, 2, s, ps);
   return total;
 }
 
@@ -1081,7 +1089,7 @@ uint64_t batchSamInto(gwa_batch_t *b, char **buf, uint64_t *cap) {
     if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
     return 0;
   }
-  const uint64_t total = formatOnDevice(b, nullptr, 0, b->n);
+  const uint64_t total = formatOnDevice(b, nullptr, 0, b->pairs ? b->pairs : b->n);
   if (*cap < total) {
     if (*buf) (void)hipHostFree(*buf);
     *buf = nullptr;
@@ -1111,11 +1119,61 @@ int gwa_batch_stats(gwa_batch_t *b, gwa_batch_stats_t *st) {
   }
 }
 
-int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) { return gwa_batch_results_range(b, 0, b->n, out); }
+int gwa_batch_format(gwa_batch_t *b, uint64_t *sam_bytes) {
+  try {
+    *sam_bytes = b->headerOnly ? 0 : formatOnDevice(b, nullptr, 0, b->pairs ? b->pairs : b->n);
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
+
+int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out) {
+  return gwa_batch_results_range(b, 0, b->pairs ? b->pairs : b->n, out);
+}
+
+int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *mate1, const gwa_reads_t *mate2,
+                           int32_t min_insert, int32_t max_insert, gwa_batch_t **out) {
+  try {
+    if (mate1->n != mate2->n) throw std::runtime_error("paired-end: the mate files hold different numbers of reads");
+    if ((mate1->qual == nullptr) != (mate2->qual == nullptr)) throw std::runtime_error("paired-end: qualities for one mate only");
+    if (cfg->strategy != 0) throw std::runtime_error("paired-end alignment runs the -m bsf search");
+    if (min_insert < 0 || max_insert < min_insert) throw std::runtime_error("bad insert-size range");
+    // one batch of 2n single-end reads: mate 1 of every pair, then mate 2
+    const uint32_t n = mate1->n;
+    std::string blob[3];
+    std::vector<uint64_t> off[3];
+    const gwa_reads_t *ms[2] = {mate1, mate2};
+    for (int f = 0; f < 3; ++f) {
+      if (f == 2 && !mate1->qual) break;
+      off[f].reserve(2 * (size_t)n + 1);
+      off[f].push_back(0);
+      for (int k = 0; k < 2; ++k) {
+        const gwa_reads_t *r = ms[k];
+        const char *base = f == 0 ? r->name : f == 1 ? r->seq : r->qual;
+        const uint64_t *o = f == 0 ? r->name_off : f == 1 ? r->seq_off : r->qual_off;
+        blob[f].append(base + o[0], o[n] - o[0]);
+        const uint64_t at = off[f].back();
+        for (uint32_t i = 1; i <= n; ++i) off[f].push_back(at + (o[i] - o[0]));
+      }
+    }
+    gwa_reads_t both{2 * n, blob[0].data(), blob[1].data(), mate1->qual ? blob[2].data() : nullptr, off[0].data(),
+                     off[1].data(), mate1->qual ? off[2].data() : nullptr};
+    gwa_config_t c = *cfg;
+    c.report_type = 1;  // every best hit of a mate is a pairing candidate
+    if (gwa_batch_create(ix, &c, &both, out) != 0) return -1;
+    (*out)->pairs = n;
+    (*out)->minIns = min_insert;
+    (*out)->maxIns = max_insert;
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
 
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out) {
   try {
-    if ((uint64_t)first + count > b->n) throw std::runtime_error("result range out of bounds");
+    if ((uint64_t)first + count > (b->pairs ? b->pairs : b->n)) throw std::runtime_error("result range out of bounds");
     formatResults(b, nullptr, first, count, out);
     return 0;
   } catch (std::exception &e) {
@@ -1126,7 +1184,7 @@ int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_
 int gwa_batch_results_select(gwa_batch_t *b, const uint32_t *idx, uint32_t count, gwa_results_t *out) {
   try {
     for (uint32_t j = 0; j < count; ++j)
-      if (idx[j] >= b->n) throw std::runtime_error("result index out of bounds");
+      if (idx[j] >= (b->pairs ? b->pairs : b->n)) throw std::runtime_error("result index out of bounds");
     formatResults(b, idx, 0, count, out);
     return 0;
   } catch (std::exception &e) {
@@ -1273,6 +1331,16 @@ int gwa_results_records(const gwa_index_t *ix, gwa_results_t *r) {
   } catch (std::exception &e) {
     return fail(e.what());
   }
+}
+
+int gwa_align_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *mate1, const gwa_reads_t *mate2,
+                    int32_t min_insert, int32_t max_insert, gwa_results_t *out) {
+  gwa_batch_t *b = nullptr;
+  if (gwa_batch_create_pairs(ix, cfg, mate1, mate2, min_insert, max_insert, &b) != 0) return -1;
+  int rc = gwa_batch_run(b);
+  if (rc == 0) rc = gwa_batch_results(b, out);
+  gwa_batch_free(b);
+  return rc;
 }
 
 int gwa_align_batch(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_results_t *out) {

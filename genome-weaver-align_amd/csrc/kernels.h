@@ -34,9 +34,13 @@ void launchEncode(const char *seq, const uint64_t *seqB, const uint64_t *seqE, u
 void launchFastqFields(const char *text, uint64_t len, const uint64_t *start, uint32_t n, uint64_t *fields,
                        uint32_t *err, hipStream_t s);
 size_t encodeScanTempBytes(uint32_t n);
+struct PairSpec {  // paired-end formatting: np pairs (mate 1 = read i, mate 2 = read np + i); np = 0: single-end
+  uint32_t np;
+  int32_t minIns, maxIns;
+};
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
                      uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
-                     uint32_t *err, char *out, int pass, hipStream_t s);
+                     uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps);
 size_t samScanTempBytes(uint32_t n);
 void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipStream_t s);
 size_t laneBytesFor(int R, const Caps &c);  // per-lane slice

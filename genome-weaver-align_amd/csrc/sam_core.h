@@ -351,4 +351,147 @@ GWA_HD int samRead(SamOut &o, const SamText &t, uint32_t r, const OutHeader &h, 
   return 0;
 }
 
+// ---- paired-end (config C5): the build's own design, the reference has none
+// (R/ReadReaderFactory.java:60-84); the rules are stated with their CPU restatement, oracle/
+// gwa_oracle.cpp orc_align_pairs.  Mate 1 of pair i is read i, mate 2 is read np + i; each mate was
+// aligned as a single-end read with every best hit reported (ALLHITS). ----
+
+// unclipped size of a hit's CIGAR (CIGAR.getUnclippedSize: M X D P N, A/CIGAR.java:115-131)
+GWA_HD int samRefLen(const uint16_t *cig, const OutHit &h) {
+  int l = 0;
+  for (uint32_t i = 0; i < h.cigarLen; ++i) {
+    const int t = cig[h.cigarOff + i] & 7;
+    if (t == 0 || t == 7 || t == 2 || t == 6 || t == 3) l += cig[h.cigarOff + i] >> 3;
+  }
+  return l;
+}
+
+// one mate's SAM line; h / mate = its chosen hit and its mate's (nullptr: unmapped)
+GWA_HD void samMateLine(SamOut &o, const SamText &t, uint32_t r, const OutHit *h, const uint16_t *hc, const OutHit *mate,
+                        bool first, bool proper, bool leftmost, int64_t tlenAbs, bool sameChr) {
+  int flag = 0x1 | (first ? 0x40 : 0x80);
+  if (proper) flag |= 0x2;
+  if (!h) flag |= 0x4;
+  if (!mate) flag |= 0x8;
+  if (h && h->strand == 1) flag |= 0x10;
+  if (mate && mate->strand == 1) flag |= 0x20;
+  o.bytes(t.name + t.nameB[r], t.nameE[r] - t.nameB[r]);
+  o.ch('\t');
+  o.num(flag);
+  o.ch('\t');
+  if (h) {
+    o.bytes(t.ctg + t.ctgOff[h->chr], t.ctgOff[h->chr + 1] - t.ctgOff[h->chr]);
+    o.ch('\t');
+    o.num(h->pos);
+    o.lit("\t1\t");
+    for (uint32_t i = 0; i < h->cigarLen; ++i) {
+      o.num(hc[h->cigarOff + i] >> 3);
+      o.ch(samfmt::kOp[hc[h->cigarOff + i] & 7]);
+    }
+    o.ch('\t');
+  } else {
+    o.lit("*\t0\t1\t*\t");
+  }
+  if (mate) {
+    if (h && sameChr) o.ch('=');
+    else o.bytes(t.ctg + t.ctgOff[mate->chr], t.ctgOff[mate->chr + 1] - t.ctgOff[mate->chr]);
+    o.ch('\t');
+    o.num(mate->pos);
+    o.ch('\t');
+  } else {
+    o.lit("*\t0\t");
+  }
+  o.num(h && mate && sameChr ? (leftmost ? tlenAbs : -tlenAbs) : 0);
+  o.ch('\t');
+  const bool rev = h && h->strand == 1;
+  const uint8_t *c = t.codes + t.codeOff[r];
+  const int m = (int)t.codeLen[r];
+  for (int j = 0; j < m; ++j) {
+    const uint8_t x = rev ? c[m - 1 - j] : c[j];
+    o.ch(samfmt::kSym[!rev ? (x > 4 ? 4 : x) : (x < 4 ? 3 - x : 4)]);
+  }
+  o.ch('\t');
+  if (!t.qual) {
+    o.ch('*');
+  } else {
+    const uint64_t q0 = t.qualB[r], qn = t.qualE[r] - t.qualB[r];
+    for (uint64_t j = 0; j < qn; ++j) o.ch(rev ? t.qual[q0 + qn - 1 - j] : t.qual[q0 + j]);
+  }
+  if (h) {
+    o.lit("\tNM:i:");
+    o.num(h->diff);
+    o.lit("\tXP:Z:");
+    o.ch(h->numHits == 1 ? 'U' : 'R');
+    o.lit("\tX0:i:");
+    o.num(h->numHits);
+  }
+  o.ch('\n');
+}
+
+// Pair i: choose the mates' hits (orc_align_pairs rules 1-3) and write both lines.  -1 where a
+// mate's search failed or the reference would throw.
+GWA_HD int samPair(SamOut &o, const SamText &t, uint32_t i, uint32_t np, const OutHeader *oh, const OutHit *hits,
+                   const uint16_t *cig, int32_t minIns, int32_t maxIns) {
+  const OutHeader &A = oh[i], &B = oh[np + i];
+  if ((A.status != ST_MAPPED && A.status != ST_UNMAPPED) || (B.status != ST_MAPPED && B.status != ST_UNMAPPED)) return -1;
+  const OutHit *ha = hits + A.hitOff, *hb = hits + B.hitOff;
+  const uint16_t *ca = cig + A.cigOff, *cb = cig + B.cigOff;
+  const int na = A.status == ST_MAPPED ? A.nChains : 0, nb = B.status == ST_MAPPED ? B.nChains : 0;
+  // candidates: the chain heads without a split and with a contig, in report order
+  const OutHit *a = nullptr, *b = nullptr, *fa = nullptr, *fb = nullptr;
+  int best = 0x7FFFFFFF;
+  for (int x = 0, hx = 0; x < na; ++x) {
+    const OutHit &u = ha[hx];
+    int e = hx;
+    while (ha[e].next >= 0) e = ha[e].next;
+    const int next = e + 1;
+    if (u.next < 0 && u.chr >= 0) {
+      if (!fa) fa = &u;
+      for (int y = 0, hy = 0; y < nb; ++y) {
+        const OutHit &v = hb[hy];
+        int f = hy;
+        while (hb[f].next >= 0) f = hb[f].next;
+        const int nextB = f + 1;
+        if (v.next < 0 && v.chr >= 0 && t.chrKey[u.chr] == t.chrKey[v.chr] && u.strand != v.strand) {
+          const OutHit &fw = u.strand == 0 ? u : v, &rv = u.strand == 0 ? v : u;
+          const uint16_t *rc = u.strand == 0 ? cb : ca;
+          const int64_t fs = fw.pos, re = (int64_t)rv.pos + samRefLen(rc, rv) - 1;
+          const int64_t tl = re - fs + 1;
+          if (!(fs > re || tl < minIns || tl > maxIns) && u.diff + v.diff < best) {
+            best = u.diff + v.diff;
+            a = &u;
+            b = &v;
+          }
+        }
+        hy = nextB;
+      }
+    }
+    hx = next;
+  }
+  if (!fb)
+    for (int y = 0, hy = 0; y < nb; ++y) {
+      const OutHit &v = hb[hy];
+      if (v.next < 0 && v.chr >= 0) { fb = &v; break; }
+      int f = hy;
+      while (hb[f].next >= 0) f = hb[f].next;
+      hy = f + 1;
+    }
+  const bool proper = a != nullptr;
+  if (!proper) {
+    a = fa;
+    b = fb;
+  }
+  const bool sameChr = a && b && t.chrKey[a->chr] == t.chrKey[b->chr];
+  int64_t tlen = 0;
+  bool aLeft = true;
+  if (sameChr) {
+    const int64_t ea = (int64_t)a->pos + samRefLen(ca, *a) - 1, eb = (int64_t)b->pos + samRefLen(cb, *b) - 1;
+    tlen = (ea > eb ? ea : eb) - (a->pos < b->pos ? a->pos : b->pos) + 1;
+    aLeft = a->pos <= b->pos;
+  }
+  samMateLine(o, t, i, a, ca, b, true, proper, aLeft, tlen, sameChr);
+  samMateLine(o, t, np + i, b, cb, a, false, proper, !aLeft, tlen, sameChr);
+  return 0;
+}
+
 }  // namespace gwa

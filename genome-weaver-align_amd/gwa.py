@@ -71,8 +71,8 @@ _lib = None
 EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_index_build_fasta", "gwa_index_open",
            "gwa_index_build_codes", "gwa_index_save", "gwa_index_text_size", "gwa_index_device_bytes", "gwa_index_export_sa",
            "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
-           "gwa_batch_create", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
-           "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_results_records", "gwa_batch_results_select",
+           "gwa_batch_create", "gwa_batch_create_pairs", "gwa_align_pairs", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
+           "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_results_records", "gwa_batch_results_select", "gwa_batch_format",
            "gwa_pipeline_open", "gwa_pipeline_align", "gwa_pipeline_align_file", "gwa_pipeline_stats",
            "gwa_pipeline_close", "gwa_reads_parse", "gwa_reads_free"]
 
@@ -103,12 +103,15 @@ def lib():
         L.gwa_free.argtypes = [V]
         L.gwa_batch_create.argtypes = [V, P(_Config), P(_Reads), P(V)]
         L.gwa_batch_run.argtypes = [V]
+        L.gwa_batch_create_pairs.argtypes = [V, P(_Config), P(_Reads), P(_Reads), ctypes.c_int32, ctypes.c_int32, P(V)]
+        L.gwa_align_pairs.argtypes = [V, P(_Config), P(_Reads), P(_Reads), ctypes.c_int32, ctypes.c_int32, P(_Results)]
         L.gwa_batch_stats.argtypes = [V, P(BatchStats)]
         L.gwa_batch_results.argtypes = [V, P(_Results)]
         L.gwa_batch_free.argtypes = [V]
         L.gwa_batch_read_counters.argtypes = [V, V]
         L.gwa_batch_results_range.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, P(_Results)]
         L.gwa_batch_results_select.argtypes = [V, V, ctypes.c_uint32, P(_Results)]
+        L.gwa_batch_format.argtypes = [V, P(U64)]
         L.gwa_reads_parse.argtypes = [ctypes.c_char_p, U64, I, I, P(_ReadBuf), P(U64)]
         L.gwa_reads_free.argtypes = [P(_ReadBuf)]
         L.gwa_pipeline_open.argtypes = [V, I, P(_Config), ctypes.c_uint32, I, P(V)]
@@ -372,6 +375,30 @@ class SuffixFilter(BidirectionalSuffixFilter):
         super().__init__(fmIndex, dataclasses.replace(config or AlignmentConfig(), strategy="sf"))
 
 
+class PairedEndAligner:
+    """Paired-end alignment (config C5) on one GPU: mate1[i] and mate2[i] form pair i; two SAM lines
+    per pair (include/gwa.h gwa_align_pairs; the build's own pairing rules -- the reference's
+    paired-end path is a stub, R/ReadReaderFactory.java:60-84, WeaverAlign.scala:259-278)."""
+
+    def __init__(self, fmIndex, config=None, min_insert=210, max_insert=390):
+        self.fmIndex = fmIndex
+        self.config = config or AlignmentConfig()
+        self.min_insert, self.max_insert = min_insert, max_insert
+
+    def align_pairs(self, mates1, mates2):
+        """mates: lists of (name, seq, qual-or-None) -> SAM text (no header), pair order."""
+        keep = []
+        r1, r2 = _reads_struct(mates1, keep), _reads_struct(mates2, keep)
+        return self.align_pair_structs(r1, r2)
+
+    def align_pair_structs(self, r1, r2):
+        res = _Results()
+        c = self.config._c()
+        _check(lib().gwa_align_pairs(self.fmIndex.h, ctypes.byref(c), ctypes.byref(r1), ctypes.byref(r2),
+                                     self.min_insert, self.max_insert, ctypes.byref(res)))
+        return _take_results(res)[0]
+
+
 class BidirectionalBWT(BidirectionalSuffixFilter):
     """`-m bd` / `-m bwa` (S/BidirectionalBWT.java): the reference reports BWAState / AlignmentSA
     objects that SAMOutput.emit drops (A/SAMOutput.java:73-82), so its SAM holds the header only;
@@ -457,8 +484,20 @@ def reads_from_blobs(name_blob, name_off, seq_blob, seq_off, qual_blob=None, qua
 class Batch:
     """Split form for benchmarking: reads resident in HBM, run() = the timed kernels."""
 
-    def __init__(self, fmIndex, config, reads=None, blobs=None):
+    def __init__(self, fmIndex, config, reads=None, blobs=None, pair_blobs=None, insert=(210, 390)):
+        """reads: [(name, seq, qual)] or blobs = (name, name_off, seq, seq_off, qual, qual_off); pair_blobs =
+        (mate-1 blobs, mate-2 blobs) makes a paired-end batch (gwa_batch_create_pairs)."""
         self._keep = []
+        self.h = ctypes.c_void_p()
+        c = config._c()
+        if pair_blobs is not None:
+            self._keep.append(pair_blobs)
+            r1, r2 = reads_from_blobs(*pair_blobs[0]), reads_from_blobs(*pair_blobs[1])
+            self.n = r1.n
+            self.n_reads = 2 * r1.n
+            _check(lib().gwa_batch_create_pairs(fmIndex.h, ctypes.byref(c), ctypes.byref(r1), ctypes.byref(r2),
+                                                insert[0], insert[1], ctypes.byref(self.h)))
+            return
         if blobs is not None:
             self._keep.append(blobs)
             r = reads_from_blobs(*blobs)
@@ -466,12 +505,16 @@ class Batch:
         else:
             r = _reads_struct(reads, self._keep)
             self.n = len(reads)
-        self.h = ctypes.c_void_p()
-        c = config._c()
         _check(lib().gwa_batch_create(fmIndex.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(self.h)))
 
     def run(self):
         _check(lib().gwa_batch_run(self.h))
+
+    def format_device(self):
+        """Write the batch's SAM text in HBM only (pairing included for paired batches); its size."""
+        n = ctypes.c_uint64()
+        _check(lib().gwa_batch_format(self.h, ctypes.byref(n)))
+        return n.value
 
     def stats(self):
         st = BatchStats()
@@ -524,7 +567,7 @@ class Batch:
         search_blocks, states, sa_reads, n_hits, quick-scan mismatches/starts x4, deepest tier, k-mer lookups,
         quick short steps, search text steps, DP verifications, verify bytes"""
         import numpy as np
-        out = np.zeros((self.n, self.READ_COUNTERS), dtype=np.int32)
+        out = np.zeros((getattr(self, "n_reads", self.n), self.READ_COUNTERS), dtype=np.int32)
         _check(lib().gwa_batch_read_counters(self.h, out.ctypes.data))
         return out
 

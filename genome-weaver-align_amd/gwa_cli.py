@@ -96,7 +96,7 @@ def build_parser():
     a = sub.add_parser("align", help="read alignment")
     a.add_argument("-r", dest="refSeq", required=True, help="reference sequence (FASTA)")
     a.add_argument("-q", dest="query", help="single query sequence")
-    a.add_argument("readFiles", nargs="*", help="read file (single-end)")
+    a.add_argument("readFiles", nargs="*", help="read file (single-end), or two mate files (paired-end)")
     a.add_argument("--silent", action="store_true", help="disable output")
     a.add_argument("-m", dest="strategy", default="bsf", help="alignment strategy: bsf (default), sf, bd, bwa")
     a.add_argument("-R", dest="reportType", default="besthit", help="besthit (default), allhits, topL")
@@ -122,6 +122,8 @@ def build_parser():
     b.add_argument("--device", type=int, default=0)
     a.add_argument("--batch", type=int, default=1 << 20, help="reads per device batch")
     a.add_argument("--timing", action="store_true", help="index / align wall times and reads/s on stderr")
+    a.add_argument("--insert-min", type=int, default=210, help="paired-end: smallest template length of a proper pair")
+    a.add_argument("--insert-max", type=int, default=390, help="paired-end: largest template length of a proper pair")
     return ap
 
 
@@ -169,11 +171,12 @@ def load_indexes(ref, devices):
 def align(ns, out=sys.stdout):
     if ns.query is None and not ns.readFiles:
         raise gwa.GwaError("no query is given")
-    if ns.query is None and len(ns.readFiles) != 1:
-        raise gwa.GwaError("# of input read files must be one (single-end)")
+    if ns.query is None and len(ns.readFiles) not in (1, 2):
+        raise gwa.GwaError("give one read file (single-end) or two mate files (paired-end)")
     cfg = config_of(ns)
     if ns.query is None:
-        _kind(ns.readFiles[0])  # unsupported suffixes fail before the index is built
+        for f in ns.readFiles:
+            _kind(f)  # unsupported suffixes fail before the index is built
     devices = [int(x) for x in ns.devices.split(",")] if ns.devices else [ns.device]
     t0 = time.perf_counter()
     fms = load_indexes(ns.refSeq, devices)
@@ -185,6 +188,8 @@ def align(ns, out=sys.stdout):
         if ns.query is not None:
             w(gwa.aligner(fms[0], cfg).align_batch([("read", ns.query, None)]))
             n = 1
+        elif len(ns.readFiles) == 2:
+            n = align_pairs(ns, fms[0], cfg, w)
         else:
             out.flush()
             pipe = gwa.Pipeline(fms, cfg, batch_reads=ns.batch, workers_per_device=ns.workers)
@@ -221,6 +226,30 @@ def align(ns, out=sys.stdout):
         print("[gwa] index load %.2fs (%d device(s)); align (read file -> SAM, index load excluded) %.2fs: %.0f reads/s"
               % (t1 - t0, len(devices), t2 - t1, n / max(t2 - t1, 1e-9)), file=sys.stderr)
     return n
+
+
+def align_pairs(ns, fm, cfg, w):
+    """Paired-end: mate i of the first file with mate i of the second (gwa_align_pairs, one GPU),
+    two SAM lines per pair.  The reference prints only the header for two read files: its paired
+    reader is a stub (R/ReadReaderFactory.java:60-84); the pairing rules are this build's own
+    (include/gwa.h gwa_batch_create_pairs)."""
+    if cfg.strategy.lower() != "bsf":
+        raise gwa.GwaError("paired-end alignment runs -m bsf")
+    pe = gwa.PairedEndAligner(fm, cfg, ns.insert_min, ns.insert_max)
+    opener = [gzip.open if f.endswith(".gz") else open for f in ns.readFiles]
+    with opener[0](ns.readFiles[0], "rb") as f1, opener[1](ns.readFiles[1], "rb") as f2:
+        p1 = gwa.ParsedReads(f1.read(), _kind(ns.readFiles[0]))
+        p2 = gwa.ParsedReads(f2.read(), _kind(ns.readFiles[1]))
+    try:
+        if p1.n != p2.n:
+            raise gwa.GwaError("the mate files hold %d and %d reads" % (p1.n, p2.n))
+        for i in range(0, p1.n, ns.batch):
+            c = min(ns.batch, p1.n - i)
+            w(pe.align_pair_structs(p1.slice(i, c), p2.slice(i, c)))
+        return p1.n
+    finally:
+        p1.close()
+        p2.close()
 
 
 def bwt(ns):

@@ -150,8 +150,22 @@ void gwa_reads_free(gwa_read_buf_t *b);
  * then fetch results. */
 int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *reads, gwa_batch_t **out);
 int gwa_batch_run(gwa_batch_t *b);
+/* Paired-end batch (config C5; the build's own design -- the reference has no paired-end path,
+ * R/ReadReaderFactory.java:60-84): mate1[i] and mate2[i] form pair i.  Each mate is aligned as a
+ * single-end read (-m bsf, every best hit kept); the pair of hits on one contig, opposite strands,
+ * forward-reverse, with template length in [min_insert, max_insert] and the fewest differences wins
+ * (rules: oracle/gwa_oracle.cpp orc_align_pairs).  Results hold two SAM lines per pair (n_reads =
+ * pairs, line_off per pair) with mate fields and TLEN. */
+int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *mate1, const gwa_reads_t *mate2,
+                           int32_t min_insert, int32_t max_insert, gwa_batch_t **out);
+/* One call per paired batch: create_pairs + run + results. */
+int gwa_align_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *mate1, const gwa_reads_t *mate2,
+                    int32_t min_insert, int32_t max_insert, gwa_results_t *out);
 int gwa_batch_stats(gwa_batch_t *b, gwa_batch_stats_t *st);
 int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out);
+/* The batch's SAM text written in HBM only (paired-end: pairing included); *sam_bytes = its size.
+ * For timing the device side of the reporting path; gwa_batch_results copies the text out. */
+int gwa_batch_format(gwa_batch_t *b, uint64_t *sam_bytes);
 /* SAM for reads [first, first+count) only (n_reads = count). */
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out);
 void gwa_batch_free(gwa_batch_t *b);

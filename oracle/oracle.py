@@ -79,6 +79,8 @@ def lib():
         L.orc_fast_count.restype = ctypes.c_int64
         L.orc_fast_count.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
         L.orc_revcomp.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.orc_align_pairs.argtypes = [ctypes.c_void_p, ctypes.POINTER(OrcConfig), ctypes.c_uint32] + [ctypes.c_void_p] * 6 + [
+            ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
         L.orc_check_cyclic_sa.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                           ctypes.c_uint64, ctypes.c_int]
         _lib = L
@@ -183,6 +185,27 @@ class Index:
         s = ctypes.string_at(out, ln.value).decode()
         lib().orc_free(out)
         return (s, stats) if with_stats else s
+
+    def align_pairs(self, mates1, mates2, config=None, min_insert=210, max_insert=390):
+        """Paired-end SAM of (name, seq, qual-or-None) mate lists (the build's own pairing rules,
+        orc_align_pairs; parity unpinned against the reference, which has no paired-end path)."""
+        n = len(mates1)
+        assert len(mates2) == n
+        arrs = []
+        for ms in (mates1, mates2):
+            arrs.append((ctypes.c_char_p * n)(*[r[0].encode() for r in ms]))
+            arrs.append((ctypes.c_char_p * n)(*[r[1].encode() for r in ms]))
+            arrs.append((ctypes.c_char_p * n)(*[(r[2].encode() if r[2] is not None else None) for r in ms]))
+        cfg = config or OrcConfig.default()
+        out = ctypes.c_void_p()
+        ln = ctypes.c_uint64()
+        rc = lib().orc_align_pairs(self.h, ctypes.byref(cfg), n, *[ctypes.cast(a, ctypes.c_void_p) for a in arrs],
+                                   min_insert, max_insert, ctypes.byref(out), ctypes.byref(ln))
+        if rc != 0:
+            raise RuntimeError("oracle align_pairs failed: " + _err())
+        s = ctypes.string_at(out, ln.value).decode()
+        lib().orc_free(out)
+        return s
 
     def backward_search(self, window, ch, lb, ub):
         a = ctypes.c_int64()

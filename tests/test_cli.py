@@ -234,3 +234,24 @@ def test_cli_malformed_fastq_reports_the_record(tmp_path):
     ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), str(rp)])
     with pytest.raises(gwa.GwaError, match="malformed FASTQ record"):
         gwa_cli.align(ns, out=io.StringIO())
+
+
+@pytest.mark.gpu
+def test_cli_paired_end_files(tmp_path):
+    import oracle as O
+    import synth
+    codes, names, lengths = synth.genome([("chrA", 60000), ("chr2", 41000)], config_id=9)
+    ref = tmp_path / "ref.fa"
+    ref.write_text(synth.fasta_text(codes, names, lengths))
+    m1, m2 = synth.pairs_codes(codes, lengths, 600, config_id=16)
+    s1, s2 = synth.to_strings(m1), synth.to_strings(m2)
+    r1 = [("q%d" % i, s1[i], "I" * 100) for i in range(600)]
+    r2 = [("q%d" % i, s2[i], "I" * 100) for i in range(600)]
+    for path, rs in ((tmp_path / "r_1.fq", r1), (tmp_path / "r_2.fq", r2)):
+        path.write_text("".join("@%s\n%s\n+\n%s\n" % r for r in rs))
+    out = io.StringIO()
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-k", "2", "--batch", "250",
+                                            str(tmp_path / "r_1.fq"), str(tmp_path / "r_2.fq")])
+    assert gwa_cli.align(ns, out=out) == 600
+    oi = O.Index.from_fasta(ref.read_text())
+    assert out.getvalue() == oi.sam_header() + oi.align_pairs(r1, r2, O.OrcConfig.default(k=2.0))

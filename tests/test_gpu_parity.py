@@ -409,3 +409,39 @@ def test_results_records_rebuild_the_sam(repetitive_pair):
     assert any(r.split >= 0 for r in recs) and any(r.ref < 0 for r in recs)
     rebuilt = [_to_sam_line(sam, names, r, recs[r.split] if r.split >= 0 else None) for r in recs if not r.is_split]
     assert "\n".join(rebuilt) + "\n" == sam
+
+
+# ---- paired-end (config C5; the build's own pairing, checked against the oracle's restatement) ----
+
+def _pairs(codes, lengths, n, seed):
+    m1, m2 = synth.pairs_codes(codes, lengths, n, config_id=seed)
+    s1, s2 = synth.to_strings(m1), synth.to_strings(m2)
+    return ([("p%d/1" % i, s1[i], "I" * 100) for i in range(n)], [("p%d/2" % i, s2[i], "J" * 100) for i in range(n)])
+
+
+@pytest.mark.parametrize("genome", ["random", "repetitive"])
+def test_paired_end_matches_oracle(random_pair, repetitive_pair, genome):
+    import gwa
+    if genome == "random":
+        codes, names, lengths, gi, oi = random_pair
+    else:
+        codes, gi, oi = repetitive_pair
+        lengths = [len(codes) // 3, len(codes) // 3, len(codes) - 2 * (len(codes) // 3)]
+    r1, r2 = _pairs(codes, lengths, 2000, 51)
+    got = gwa.PairedEndAligner(gi, gwa.AlignmentConfig(k=2.0)).align_pairs(r1, r2)
+    exp = oi.align_pairs(r1, r2, O.OrcConfig.default(k=2.0))
+    assert got == exp
+    flags = [int(l.split("\t")[1]) for l in got.splitlines()]
+    # proper pairs: most on the random genome; on the repetitive one a multi-hit mate reports one position
+    assert len(flags) == 4000 and sum(1 for f in flags if f & 0x2) > (3000 if genome == "random" else 1000)
+
+
+def test_paired_end_insert_window_and_unmapped_mates(random_pair):
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    r1, r2 = _pairs(codes, lengths, 500, 52)
+    rng = np.random.default_rng(53)
+    # some mates unmappable, a narrow insert window (most pairs fail it)
+    r2 = [(n, "".join(rng.choice(list("ACGT"), 100)) if i % 7 == 0 else s, q) for i, (n, s, q) in enumerate(r2)]
+    got = gwa.PairedEndAligner(gi, gwa.AlignmentConfig(k=2.0), 295, 305).align_pairs(r1, r2)
+    assert got == oi.align_pairs(r1, r2, O.OrcConfig.default(k=2.0), 295, 305)

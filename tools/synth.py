@@ -228,6 +228,44 @@ def reads_codes(codes, lengths, n, m=100, max_subs=2, config_id=2, shard=0, inde
     return out
 
 
+def pairs_codes(codes, lengths, n, m=100, mean=300, sd=30, max_subs=2, config_id=5, shard=0):
+    """Paired-end reads (config C5): fragment length ~ N(mean, sd) (at least m), start uniform over
+    N-free fragment windows; mate 1 = the fragment's first m bases and mate 2 = the reverse complement
+    of its last m (or, for half the pairs, the fragment of the other strand: mates swapped and both
+    reverse-complemented); each mate gets uniform {0..max_subs} substitutions.
+    -> (mate1 codes uint8 [n, m], mate2 codes uint8 [n, m])."""
+    rng = np.random.Generator(np.random.PCG64((SEED0 ^ config_id) + shard))
+    N = len(codes)
+    offs = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    L = np.array(lengths, dtype=np.int64)
+    flen = np.maximum(m, np.rint(rng.normal(mean, sd, n))).astype(np.int64)
+    W = int(flen.max())
+    p = np.where(L >= W + 2, L - W - 1, 0).astype(np.float64)
+    p /= p.sum()
+    ci = rng.choice(len(L), size=n, p=p)
+    starts = offs[ci] + (rng.random(n) * (L[ci] - W - 1)).astype(np.int64)
+    for _ in range(64):  # N-free fragments
+        win = codes[np.minimum(starts[:, None] + np.arange(W)[None, :], N - 1)]
+        bad = np.nonzero(((win == 4) & (np.arange(W)[None, :] < flen[:, None])).any(axis=1))[0]
+        if len(bad) == 0:
+            break
+        cj = rng.choice(len(L), size=len(bad), p=p)
+        starts[bad] = offs[cj] + (rng.random(len(bad)) * (L[cj] - W - 1)).astype(np.int64)
+    a = codes[starts[:, None] + np.arange(m)[None, :]]
+    b = codes[(starts + flen - m)[:, None] + np.arange(m)[None, :]]
+    b = COMP[b[:, ::-1]]
+    swap = rng.integers(0, 2, n).astype(bool)
+    m1 = np.where(swap[:, None], b, a)
+    m2 = np.where(swap[:, None], a, b)
+    for mate in (m1, m2):
+        nsub = rng.integers(0, max_subs + 1, n)
+        for j in range(max_subs):
+            rows = np.nonzero(nsub > j)[0]
+            pos = rng.integers(0, m, len(rows))
+            mate[rows, pos] = (mate[rows, pos] + rng.integers(1, 4, len(rows)).astype(np.uint8)) % 4
+    return m1, m2
+
+
 def name_blob(n, start=0):
     """names r%09d as one bytes blob + offsets (10 bytes each)."""
     ids = np.arange(start, start + n, dtype=np.int64)
