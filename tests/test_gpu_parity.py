@@ -445,3 +445,16 @@ def test_paired_end_insert_window_and_unmapped_mates(random_pair):
     r2 = [(n, "".join(rng.choice(list("ACGT"), 100)) if i % 7 == 0 else s, q) for i, (n, s, q) in enumerate(r2)]
     got = gwa.PairedEndAligner(gi, gwa.AlignmentConfig(k=2.0), 295, 305).align_pairs(r1, r2)
     assert got == oi.align_pairs(r1, r2, O.OrcConfig.default(k=2.0), 295, 305)
+
+
+def test_gpu_cyclic_sa_known_answers(gwa):
+    # the GPU suffix-array builder on CyclicSAISTest's texts (T/sais/CyclicSAISTest.java:45-90),
+    # relabelled order-preservingly to the index alphabet
+    import json
+    from test_oracle_golden import _relabel
+    G = json.load(open(os.path.join(HERE, "golden", "reference_known_answers.json")))
+    for case in G["cyclic_sa"]:
+        codes = np.array(_relabel(case["text"]), dtype=np.uint8)
+        gi = gwa.FMIndexOnGenome.buildFromCodes(codes, ["t"], [len(codes)])
+        assert list(gi.suffixArray(0)) == case["expect"], case["name"]
+        gi.close()

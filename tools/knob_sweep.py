@@ -23,8 +23,12 @@ def main():
     import numpy as np
     import synth
     import gwa
-    contigs = synth.HG19_CONTIGS if a.genome == "hg19" else [("chr%d" % (i + 1), int(float(a.genome) * 1e6 / 4)) for i in range(4)]
-    codes, names, lengths = synth.genome(contigs, config_id=1)
+    if a.genome == "hg19r":
+        codes, names, lengths = synth.genome_repeats(synth.HG19_CONTIGS, config_id=1)
+    else:
+        contigs = synth.HG19_CONTIGS if a.genome == "hg19" else [("chr%d" % (i + 1), int(float(a.genome) * 1e6 / 4))
+                                                                   for i in range(4)]
+        codes, names, lengths = synth.genome(contigs, config_id=1)
     gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths, device=0)
     m = 100
     seqs = synth.reads_codes(codes, lengths, a.reads, m, 2, config_id=2, shard=0)
