@@ -185,7 +185,8 @@ struct DHit {
 
 // per-lane scratch capacities (entries)
 struct Caps {
-  int32_t arena, heap, hits, list, cigar, dpWords, path, wr;
+  int32_t arena, heap, hits, list, cigar, dpWords, path;
+  int32_t dpSlice;  // 1: the DP history keeps a 32-row slice around the read's diagonal (first tier)
   int32_t cand;  // SuffixFilter candidate set (sf_core.h); 0 on the BSF path
 };
 
@@ -199,7 +200,7 @@ struct LaneMem {
   uint8_t *slice;          // this lane's slice: arena | heap | hits | list | cigar
   uint8_t *chunk;          // interleaved block (the wavefront's on the GPU, the lane's on the host)
   uint32_t oHeap, oCand, oHits, oList, oCigar;  // byte offsets in the slice
-  uint32_t oWr, oPath;     // byte offsets of the wr / path planes in the chunk
+  uint32_t oPath;          // byte offset of the path plane in the chunk
   int lane, is;            // lane in the interleaved block, interleave stride (elements)
   // PriorityQueue array of (key << 16 | state index): entry i at heapP[i * hs].  In the slice
   // (hs = 1) or, for the first tier, in LDS interleaved across the workgroup (hs = 256)
@@ -212,7 +213,6 @@ struct LaneMem {
   GWA_HD int32_t *list() const { return (int32_t *)(slice + oList); }
   GWA_HD uint16_t *cigar() const { return (uint16_t *)(slice + oCigar); }
   GWA_HD uint64_t *dp() const { return (uint64_t *)chunk + lane; }   // [2][col 0..N][block] vp / vn history
-  GWA_HD uint8_t *wr() const { return chunk + oWr + lane; }          // [col 0..N] blocks computed (bits 0-3) / activated (4-7)
   GWA_HD uint8_t *path() const { return chunk + oPath + lane; }      // traceback path
 };
 
@@ -228,7 +228,7 @@ GWA_HD size_t laneBytes(const Caps &c) {  // per-lane slice
   return (b + 255) & ~(size_t)255;
 }
 GWA_HD size_t ilvBytes(const Caps &c) {  // interleaved bytes per lane
-  return (8 * (size_t)c.dpWords + (size_t)c.wr + (size_t)c.path + 7) & ~(size_t)7;
+  return (8 * (size_t)c.dpWords + (size_t)c.path + 7) & ~(size_t)7;
 }
 
 // slice = this lane's slice; chunk = its wavefront's interleaved block (64 lanes, is = 64), or the
@@ -244,8 +244,7 @@ GWA_HD LaneMem<R> laneMem(uint8_t *slice, uint8_t *chunk, int laneInWave, int is
   L.oList = (uint32_t)b; b += 4 * (size_t)c.list;
   L.oCigar = (uint32_t)b;
   L.chunk = chunk;
-  L.oWr = (uint32_t)((size_t)is * 8 * c.dpWords);
-  L.oPath = (uint32_t)((size_t)is * (8 * (size_t)c.dpWords + (size_t)c.wr));
+  L.oPath = (uint32_t)((size_t)is * 8 * (size_t)c.dpWords);
   L.lane = laneInWave;
   L.is = is;
   L.heapP = (uint64_t *)(slice + L.oHeap);
@@ -287,6 +286,34 @@ struct RefCursor {
       xn = tn[nb];
     }
     return ((cn >> (p & 63)) & 1) ? 4 : (int)((c2 >> ((p & 31) * 2)) & 3);
+  }
+};
+
+// The DP's reference window [p0, p0 + n) held in registers: 2-bit codes as W2 words of 32 bases and
+// the N bitmap as WN words of 64, each re-aligned to p0 (funnel shift).  All 2 (W2 + WN + 2) loads are
+// issued together before the DP, so the window costs one memory wait; RefCursor's per-column
+// prefetch made every column of a wavefront wait on whichever lane crossed a word boundary.
+template <int W2, int WN>
+struct RefWindow {
+  uint64_t c2[W2], cn[WN];
+  GWA_HD void load(const uint64_t *t2, const uint64_t *tn, uint64_t N, int64_t p0) {
+    const int64_t last2 = N ? (int64_t)((N - 1) >> 5) : 0, lastN = N ? (int64_t)((N - 1) >> 6) : 0;
+    const int64_t a = p0 >> 5, b = p0 >> 6;
+    uint64_t r2[W2 + 1], rn[WN + 1];
+#pragma unroll
+    for (int i = 0; i <= W2; ++i) r2[i] = t2[a + i < last2 ? a + i : last2];
+#pragma unroll
+    for (int i = 0; i <= WN; ++i) rn[i] = tn[b + i < lastN ? b + i : lastN];
+    const int s2 = (int)(p0 & 31) * 2, sn = (int)(p0 & 63);
+#pragma unroll
+    for (int i = 0; i < W2; ++i) c2[i] = s2 ? (r2[i] >> s2) | (r2[i + 1] << (64 - s2)) : r2[i];
+#pragma unroll
+    for (int i = 0; i < WN; ++i) cn[i] = sn ? (rn[i] >> sn) | (rn[i + 1] << (64 - sn)) : rn[i];
+  }
+  // code (0-3, 4 = N) of window position j (0 <= j < 32 * W2)
+  GWA_HD int code(int j) const {
+    if ((pick(cn, j >> 6) >> (j & 63)) & 1) return 4;
+    return (int)((pick(c2, j >> 5) >> ((j & 31) * 2)) & 3);
   }
 };
 
@@ -1150,6 +1177,13 @@ struct BsfLane {
   // computed, 4-7 activated-as-input; cells never written read as 0, as the reference's
   // zero-initialised long[][] do) is packed 4 columns to a u32 and stored once per 4 columns.
   struct alignas(16) VpVn { uint64_t vp, vn; };
+  // bits [lo, lo + 32) of a DP column of DB blocks (rows outside [0, 64 DB) read as 0)
+  GWA_HD static uint32_t rows32(const uint64_t (&E)[DB], int lo) {
+    const int w = lo >> 6, sh = lo & 63;  // lo < 0: w = -1
+    const uint64_t a = w >= 0 && w < DB ? pick(E, w) : 0ULL;
+    const uint64_t b = w + 1 >= 0 && w + 1 < DB ? pick(E, w + 1) : 0ULL;
+    return (uint32_t)((a >> sh) | (sh ? b << (64 - sh) : 0ULL));
+  }
   // Peq of the DP query (the fragment q[strand][qs, qe), reversed on strand 1, :532-534) for block r
   // and base ch: bit j = (query[64 r + j] == ch), from the 2-bit read words (eqWindow), not per base
   GWA_HD uint64_t dpPeq(int strand, int qs, int qe, int r, int ch) const {
@@ -1173,7 +1207,7 @@ struct BsfLane {
     const int N = (int)(refEnd - refStart);
     ++numSW;
     verifyBytes += (2 * N + 7) / 8 + (N + 7) / 8 + 32 * bMax;
-    if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords || 4 * ((N >> 2) + 1) > caps.wr) { status = ST_OVERFLOW; return -1; }
+    if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords) { status = ST_OVERFLOW; return -1; }
     uint64_t pA[DB], pC[DB], pG[DB], pT[DB];
 #pragma unroll
     for (int r = 0; r < DB; ++r) {
@@ -1184,8 +1218,7 @@ struct BsfLane {
       pT[r] = on ? dpPeq(strand, qs, qe, r, 3) : 0ULL;
     }
     const size_t is = (size_t)L.is;
-    VpVn *hist = (VpVn *)L.chunk + L.lane;                      // [col 0..N][block] history
-    uint32_t *wr = (uint32_t *)(L.chunk + L.oWr) + L.lane;      // [col / 4] write records, byte col % 4
+    VpVn *hist = (VpVn *)L.chunk + L.lane;  // [col 0..N][block]: the value the reference's history holds
     uint64_t vp[DB], vn[DB];
     int D[DB] = {}, sb[DB];
 #pragma unroll
@@ -1195,131 +1228,203 @@ struct BsfLane {
       const int v = mq - ((r + 1) * w) + kb;
       sb[r] = v > 0 ? v : 0;
     }
-    uint32_t pend = (uint32_t)(((1 << bMax) - 1) << 4);  // column 0 inputs: ~0 / 0 for every block
-    uint32_t wacc = 0;
     D[0] = mq;
     int bCeil = (kb + w - 1) / w;
     if (bCeil < 1) bCeil = 1;
     int have = 0;  // int, not bool: see quickScan
     int bestTail = 0, bestDiff = 0;
-    RefCursor rc(ix.text2, ix.textN, ix.N);
+    // the window: N <= m + 2k + 2 <= 32 QW + 64 bases
+    RefWindow<QW + 2, QW / 2 + 1> rw;
+    if (N > 32 * (QW + 2)) { status = ST_OVERFLOW; return -1; }
+    rw.load(ix.text2, ix.textN, ix.N, refStart);
+    GWA_PT(tdf);
+    // Column c of the history holds, per block, what the reference's zero-initialised arrays hold
+    // after the whole pass: ~0 / 0 when the block was activated with input column c (the later
+    // write), else the value computed at column c - 1, else 0 / 0.  Column c is stored at the end
+    // of iteration c, once its activation is known, so the traceback reads one word per edit and
+    // nothing else (no per-column flags).
+    // First tier (caps.dpSlice): only rows [lo, lo + 32) of column c are kept, lo = c - c0 - 17
+    // around the window's middle diagonal c0 = (N - mq) / 2 (= k, the read's offset x - refStart
+    // in the window, :507, away from the text ends), as one {vp 32 | vn 32} word -- 8 B per column
+    // instead of 16 B per block.  A traceback that leaves the slice overflows the read into the
+    // next tier, which keeps whole columns.  (dpSlice - 1 shifts the slice: tests only.)
+    const bool slice = caps.dpSlice != 0;
+    const int c0 = ((N - mq) >> 1) + (slice ? caps.dpSlice - 1 : 0);
+    uint64_t *h8 = (uint64_t *)L.chunk + L.lane;
+    // (column 0, the input column, is never read: the traceback reads columns col + 1 >= 1)
+    const size_t colStep = (size_t)bMax * is;
+    VpVn *hc = hist;
+    uint64_t *hc8 = h8;
+    uint32_t comp = 0;  // blocks computed at the previous column
+    uint64_t run2 = 0, runN = 0;  // the window's codes from column j on (the loop index is uniform)
     for (int j = 0; j < N; ++j) {
-      const int ch = rc.code(refStart + j, 1);
+      if ((j & 31) == 0) run2 = pick(rw.c2, j >> 5);
+      if ((j & 63) == 0) runN = pick(rw.cn, j >> 6);
+      const int ch = (runN & 1ULL) ? 4 : (int)(run2 & 3ULL);
+      run2 >>= 2;
+      runN >>= 1;
+      // every block is computed (selects, no divergent branches): blocks past bCeil give values
+      // nobody reads, except block bCeil, whose input is set to ~0 / 0 first -- if it is activated
+      // at this column (:427-428) its carry-in is that of the active blocks above it, as there
+      uint64_t pvp[DB], pvn[DB], x[DB];
+      int nsv[DB], hinv[DB];
       int carry = 0;
-      uint32_t wmask = 0;
 #pragma unroll
       for (int r = 0; r < DB; ++r) {
-        if (r < bCeil) {
-          const uint64_t x = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
-          const int ns = dpBlock(x, carry, vp[r], vn[r]);
-          D[r] += ns;
-          carry = ns;
-          hist[((size_t)(j + 1) * bMax + r) * is] = VpVn{vp[r], vn[r]};
-          wmask |= 1u << r;
-        }
+        pvp[r] = vp[r];
+        pvn[r] = vn[r];
+        if (r == bCeil) { vp[r] = ~0ULL; vn[r] = 0ULL; }
+        x[r] = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
+        hinv[r] = carry;
+        nsv[r] = dpBlock(x[r], carry, vp[r], vn[r]);
+        if (r < bCeil) D[r] += nsv[r];
+        carry = nsv[r];
       }
+      const int bOld = bCeil;
       const int dPrev = pick(D, bCeil - 1);
-      const uint64_t nextPeq = ch == 0 ? pick(pA, bCeil) : ch == 1 ? pick(pC, bCeil) : ch == 2 ? pick(pG, bCeil) : ch == 3 ? pick(pT, bCeil) : 0ULL;
-      if (bCeil < bMax && dPrev - carry <= pick(sb, bCeil - 1) && (((nextPeq & 1ULL) != 0ULL) || carry < 0)) {
-        // activate block bCeil with input column j = ~0 / 0 (:427-428)
-        pend |= 1u << (4 + bCeil);
+      const int cIn = pick(hinv, bCeil);  // ns of block bCeil - 1
+      const uint64_t nextPeq = pick(x, bCeil);
+      const int act = bCeil < bMax && dPrev - cIn <= pick(sb, bCeil - 1) && (((nextPeq & 1ULL) != 0ULL) || cIn < 0);
+      const int actBlock = act ? bCeil : -1;
 #pragma unroll
-        for (int r = 0; r < DB; ++r) {
-          if (r == bCeil) {
-            vp[r] = ~0ULL;
-            vn[r] = 0ULL;
-            const uint64_t x = nextPeq;
-            const int ns = dpBlock(x, carry, vp[r], vn[r]);
-            D[r] = dPrev - carry + ns;
-            hist[((size_t)(j + 1) * bMax + r) * is] = VpVn{vp[r], vn[r]};
-            wmask |= 1u << r;
-          }
-        }
+      for (int r = 0; r < DB; ++r)
+        if (r == actBlock) D[r] = dPrev - cIn + nsv[r];
+      if (act) {
         bCeil++;
       } else {
-        while (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
+#pragma unroll
+        for (int q = 0; q < DB - 1; ++q)
+          if (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
       }
-      wacc |= pend << (8 * (j & 3));
-      if ((j & 3) == 3) {
-        wr[(size_t)(j >> 2) * is] = wacc;
-        wacc = 0;
+      // column j: activation wins over the value computed at j - 1
+      {
+        uint64_t ev[DB], en[DB];
+#pragma unroll
+        for (int r = 0; r < DB; ++r) {
+          const bool on = r == actBlock, cp = (comp >> r) & 1u;
+          ev[r] = on ? ~0ULL : cp ? pvp[r] : 0ULL;
+          en[r] = on ? 0ULL : cp ? pvn[r] : 0ULL;
+        }
+        if (slice) {
+          const int lo = j - c0 - 17;
+          *hc8 = (uint64_t)rows32(ev, lo) | ((uint64_t)rows32(en, lo) << 32);
+        } else {
+#pragma unroll
+          for (int r = 0; r < DB; ++r)
+            if (r < bMax) hc[r * is] = VpVn{ev[r], en[r]};
+        }
       }
-      pend = wmask;
+      hc += colStep;
+      hc8 += is;
+      comp = ((1u << bOld) - 1u) | (act ? 1u << bOld : 0u);
       if (bCeil == bMax) {
         const int dl = pick(D, bCeil - 1);
         if (!have) { have = 1; bestTail = j; bestDiff = dl; continue; }
         if (bestDiff > dl) { bestTail = j; bestDiff = dl; }
       }
     }
-    wr[(size_t)(N >> 2) * is] = wacc | (pend << (8 * (N & 3)));
+    {
+      uint64_t ev[DB], en[DB];
+#pragma unroll
+      for (int r = 0; r < DB; ++r) {
+        const bool cp = (comp >> r) & 1u;
+        ev[r] = cp ? vp[r] : 0ULL;
+        en[r] = cp ? vn[r] : 0ULL;
+      }
+      if (slice) {
+        const int lo = N - c0 - 17;
+        *hc8 = (uint64_t)rows32(ev, lo) | ((uint64_t)rows32(en, lo) << 32);
+      } else {
+#pragma unroll
+        for (int r = 0; r < DB; ++r)
+          if (r < bMax) hc[r * is] = VpVn{ev[r], en[r]};
+      }
+    }
+    GWA_PA(PR_DPF, tdf);
     (void)bestDiff;
     if (!have) return 1;
+    GWA_PT(tdt);
     // Traceback (:515-643).  A match decides the step from the codes alone (:547), so the history is
-    // read only at edits.  The path is generated backwards (CIGAR end first) and run-length encoded
-    // as it goes -- no path array: S/I/D before the first M are the trailing soft clip (`right`),
-    // S/I/D after the last M the leading one (`left`); the runs in between are kept (generation
-    // order) at the top of this read's CIGAR area, CIGAR entry cap-1-i = run i.  The ops then come
-    // out as cigarStr = reverse(path) + CIGAR.add merging would make them (:599-643).
+    // read only at edits: each round walks a lane's run of matches up its diagonal, then takes one
+    // edit step, so the lanes of a wavefront issue their history reads together (one memory latency
+    // per round, not per step).  The path is generated backwards (CIGAR end first) and run-length
+    // encoded as it goes -- no path array: S/I/D before the first M are the trailing soft clip
+    // (`right`), S/I/D after the last M the leading one (`left`); the runs in between are kept
+    // (generation order) at the top of this read's CIGAR area, CIGAR entry cap-1-i = run i.  The ops
+    // then come out as cigarStr = reverse(path) + CIGAR.add merging would make them (:599-643).
     uint16_t *cg = L.cigar();
     const int cap = caps.cigar;
     int row = mq - 1, col = bestTail;
     int diff = 0, leftMostPos = 0;
     int right = 0, adj = 0;  // trailing S/I/D count, of which I/D
     int seenM = 0, curT = 0, curL = 0, nRuns = 0, lastM = 0, pendL = 0, pendAdj = 0;
+    int bad = 0;
+    // path char t (0 M, 1 I, 2 D, 4 S), cnt of them
+    auto emit = [&](int t, int cnt) {
+      if (cnt <= 0) return;
+      if (!seenM) {
+        if (t == 0) { seenM = 1; curT = 0; curL = cnt; lastM = 0; }
+        else { right += cnt; adj += (t == 1 || t == 2) ? 1 : 0; }
+      } else {
+        if (t == curT) {
+          curL += cnt;
+        } else {
+          if (nCigar + 2 * nRuns + 4 > cap) bad = 1;
+          else cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
+          ++nRuns;
+          curT = t;
+          curL = cnt;
+        }
+        if (t == 0) { lastM = nRuns; pendL = 0; pendAdj = 0; }
+        else { pendL += cnt; pendAdj += (t == 1 || t == 2) ? 1 : 0; }
+      }
+    };
     for (;;) {
-      int t = 4, cnt = 1;  // path char of this step: 0 M, 1 I, 2 D, 4 S (cnt of them)
-      int fin = 0;
-      if (col >= 0 && row >= 0) {
-        // query base at row == reference base: the row's bit of Peq[ref base] (no read-word lookup)
-        const int rch = rc.code(refStart + col, -1);
+      // the run of matches: query base at row == reference base, the row's bit of Peq[ref base]
+      int runLen = 0;
+      int go = col >= 0 && row >= 0;
+      while (go) {
+        const int rch = rw.code(col);
         const int rb = row >> 6;
         const uint64_t pq = rch == 0 ? pick(pA, rb) : rch == 1 ? pick(pC, rb) : rch == 2 ? pick(pG, rb) : pick(pT, rb);
-        if (rch < 4 && ((pq >> (row & 63)) & 1ULL)) {
-          t = 0;
+        const int mt = rch < 4 && ((pq >> (row & 63)) & 1ULL);
+        runLen += mt;
+        col -= mt;
+        row -= mt;
+        go = mt && col >= 0 && row >= 0;
+      }
+      if (runLen > 0) {
+        leftMostPos = col + 1;
+        emit(0, runLen);
+      }
+      if (col >= 0 && row >= 0) {
+        int bp, bn;
+        if (slice) {
+          const int rr = row - (col + 1 - c0 - 17);
+          if (rr < 0 || rr >= 32) { status = ST_OVERFLOW; return -1; }  // off the slice: next tier
+          const uint64_t h = h8[(size_t)(col + 1) * is];
+          bp = (int)(h >> rr) & 1;
+          bn = (int)(h >> (32 + rr)) & 1;
         } else {
           const int block = row >> 6, offset = row & 63;
-          const uint32_t wb = (wr[(size_t)((col + 1) >> 2) * is] >> (8 * ((col + 1) & 3))) & 0xFFu;
-          uint64_t vpw = 0, vnw = 0;
-          if ((wb >> block) & 1) {  // computed at column col (the later write when both happened)
-            const VpVn h = hist[((size_t)(col + 1) * bMax + block) * is];
-            vpw = h.vp;
-            vnw = h.vn;
-            if ((wb >> (4 + block)) & 1) { vpw = ~0ULL; vnw = 0; }
-          } else if ((wb >> (4 + block)) & 1) {
-            vpw = ~0ULL;
-            vnw = 0;
-          }
-          t = (vpw >> offset) & 1 ? 1 : ((vnw >> offset) & 1) == 0 ? 0 : 2;
-          diff++;
+          const VpVn h = hist[((size_t)(col + 1) * bMax + block) * is];
+          bp = (int)(h.vp >> offset) & 1;
+          bn = (int)(h.vn >> offset) & 1;
         }
+        const int t = bp ? 1 : bn == 0 ? 0 : 2;
+        diff++;
         if (t == 0) { leftMostPos = col; col--; row--; }
         else if (t == 1) { leftMostPos = col + 1; row--; }
         else { col--; }
+        emit(t, 1);
       } else {
         // NONE: the remaining rows become S (:588-597)
-        fin = 1;
-        cnt = row >= 0 ? row + 1 : 0;
+        emit(4, row >= 0 ? row + 1 : 0);
+        break;
       }
-      if (cnt > 0) {
-        if (!seenM) {
-          if (t == 0) { seenM = 1; curT = 0; curL = 1; lastM = 0; }
-          else { right += cnt; adj += (t == 1 || t == 2) ? 1 : 0; }
-        } else {
-          if (t == curT) {
-            curL += cnt;
-          } else {
-            if (nCigar + 2 * nRuns + 4 > cap) { status = ST_OVERFLOW; return -1; }
-            cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
-            ++nRuns;
-            curT = t;
-            curL = cnt;
-          }
-          if (t == 0) { lastM = nRuns; pendL = 0; pendAdj = 0; }
-          else { pendL += cnt; pendAdj += (t == 1 || t == 2) ? 1 : 0; }
-        }
-      }
-      if (fin) break;
     }
+    if (bad) { status = ST_OVERFLOW; return -1; }
+    GWA_PA(PR_DPT, tdt);
     const int off = nCigar;
     if (!seenM) {
       diff -= adj;  // the whole path is the leading clip (left = plen, right = 0)

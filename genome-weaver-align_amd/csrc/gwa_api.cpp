@@ -834,7 +834,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       const int nref = m + 2 * b->kmax + 2;
       caps.dpWords = 2 * bMax * (nref + 1);
       caps.path = m + nref + 8;
-      caps.wr = nref + 2;
+      caps.dpSlice = t == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
       const uint64_t stride = laneBytesFor(b->R, caps);
       uint32_t lanes = std::min<uint32_t>(n, T.maxLanes);
       lanes = (lanes + 255) / 256 * 256;
@@ -868,10 +868,10 @@ int gwa_batch_run(gwa_batch_t *b) {
         for (size_t i = 0; i < pv.size(); ++i) sum[i % PR_N] += (double)pv[i];
         static const char *nm[PR_N] = {"poll", "report", "bound", "exp1", "add1", "expN", "split", "loop",
                                        "verify", "nfa", "fm", "seed", "nVerifyWave", "nVerifyLane", "nStepWave",
-                                       "nStepLane", "-", "-", "-", "wave"};
+                                       "nStepLane", "dpFwd", "dpTrace", "sumWait", "wave"};
         fprintf(stderr, "[gwa-prof] tier %d reads %u lanes %u (Gcycles summed over waves; counts in M):", t, n, lanes);
         for (int q = 0; q < PR_N; ++q)
-          if (nm[q][0] != '-') fprintf(stderr, " %s=%.2f", nm[q], sum[q] / (q >= PR_NVW && q <= PR_NSL ? 1e6 : 1e9));
+          if (nm[q][0] != '-') fprintf(stderr, " %s=%.2f", nm[q], sum[q] / ((q >= PR_NVW && q <= PR_NSL) || q == PR_NWAIT ? 1e6 : 1e9));
         fprintf(stderr, "\n");
       }
 #else

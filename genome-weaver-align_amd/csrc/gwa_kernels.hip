@@ -170,6 +170,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
     if (__ballot(phase != EXHAUSTED) == 0) break;
     const int nWait = __popcll(__ballot(phase == WAIT));
     const int nRun = __popcll(__ballot(phase == RUN));
+#ifdef GWA_PROF
+    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_NWAIT] += (uint64_t)nWait;
+#endif
     if (nWait > 0 && nWait * 16 >= cfg.waitQ16 * (nWait + nRun)) {
       if (phase == WAIT) phase = lane.searchReport() ? RUN : FINISH;
     } else if (phase == RUN) {

@@ -177,6 +177,6 @@ struct ScanRes {
 
 // CIGAR op = (len << 3) | type ; type: M0 I1 D2 N3 S4 H5 P6 X7  (A/CIGAR.java:39-47)
 // search-loop profiling regions (-DGWA_PROF builds)
-enum { PR_POLL, PR_REPORT, PR_BOUND, PR_EXP1, PR_ADD1, PR_EXPN, PR_SPLIT, PR_LOOP, PR_VERIFY, PR_NFA, PR_FM, PR_SEED, PR_NVW, PR_NVL, PR_NSW, PR_NSL, PR_N = 20 };
+enum { PR_POLL, PR_REPORT, PR_BOUND, PR_EXP1, PR_ADD1, PR_EXPN, PR_SPLIT, PR_LOOP, PR_VERIFY, PR_NFA, PR_FM, PR_SEED, PR_NVW, PR_NVL, PR_NSW, PR_NSL, PR_DPF, PR_DPT, PR_NWAIT, PR_N = 20 };
 
 }  // namespace gwa

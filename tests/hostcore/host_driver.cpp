@@ -28,13 +28,16 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
                   const char *const *names, const char *const *seqs, const char *const *quals, std::string &sam,
                   int32_t *stats) {
   const int bMax = std::max(1, (maxM + 63) / 64), nref = maxM + 2 * kmax + 2;
-  const int dpw = 2 * bMax * (nref + 1), path = maxM + nref + 8, wrn = nref + 2;
-  const Caps tiers[4] = {{256, kLdsHeap, 32, 32, 512, dpw, path, wrn, 0}, {1024, 1024, 64, 64, 1024, dpw, path, wrn, 0},
-                         {4096, 4096, 256, 256, 4096, dpw, path, wrn, 0}, {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 0}};
+  const int dpw = 2 * bMax * (nref + 1), path = maxM + nref + 8;
+  // GWA_TEST_SLICE_SHIFT moves the first tier's DP slice off the diagonal (every edit then
+  // overflows into the next tier): the slice fallback path gives the same SAM
+  const int sl = 1 + (getenv("GWA_TEST_SLICE_SHIFT") ? atoi(getenv("GWA_TEST_SLICE_SHIFT")) : 0);
+  const Caps tiers[4] = {{256, kLdsHeap, 32, 32, 512, dpw, path, sl, 0}, {1024, 1024, 64, 64, 1024, dpw, path, 0, 0},
+                         {4096, 4096, 256, 256, 4096, dpw, path, 0, 0}, {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 0}};
   // -m sf tiers (gwa_api.cpp kSfTiers)
-  const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, wrn, 32}, {2048, 2048, 64, 64, 2048, dpw, path, wrn, 256},
-                           {8192, 8192, 256, 256, 4096, dpw, path, wrn, 1024},
-                           {65536, 65536, 4096, 4096, 65536, dpw, path, wrn, 16384}};
+  const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, sl, 32}, {2048, 2048, 64, 64, 2048, dpw, path, 0, 256},
+                           {8192, 8192, 256, 256, 4096, dpw, path, 0, 1024},
+                           {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 16384}};
   std::vector<uint8_t> scratch(std::max(laneBytes<R>(tiers[3]), laneBytes<R>(sfTiers[3])) + ilvBytes(tiers[3]) + 4096);
   // one read at a time: a one-slot OutSlots whose pool is large enough for any report
   const int chains = cfg.reportType == 0 ? 1 : 2;

@@ -219,3 +219,17 @@ def test_three_piece_chimeras_two_splits():
     for m in (90, 120):
         reads = genomes.three_fragment_reads(codes, 200, m=m)
         _cmp(codes, names, lengths, reads, 5.0, num_split=2)
+
+
+@pytest.mark.parametrize("strategy", [0, 1])
+def test_dp_slice_fallback(random_genome, repetitive_genome, monkeypatch, strategy):
+    """The first tier keeps a 32-row slice of the DP history around the read's diagonal; a traceback
+    leaving it overflows the read into the next tier (whole columns).  With the slice moved off the
+    diagonal every edit takes that path, and the SAM is unchanged."""
+    monkeypatch.setenv("GWA_TEST_SLICE_SHIFT", "40")
+    codes, names, lengths = random_genome
+    seqs, rn = synth.reads(codes, lengths, 120, 150, config_id=4, indels=True, max_edits=5)
+    strs = synth.to_strings(seqs)
+    _cmp(codes, names, lengths, [(rn[i], strs[i], None) for i in range(len(strs))], 5.0, strategy=strategy)
+    codes, names, lengths = repetitive_genome
+    _cmp(codes, names, lengths, _mk(codes, 150, 100, 2, True, seed=5), 2.0, strategy=strategy)
