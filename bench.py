@@ -192,6 +192,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    win0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # the rocprofv3 trace's clock (tools/prof_summary.py)
     kms = qms = sms = 0.0
     for _ in range(args.steps):
         batch.run()
@@ -202,6 +203,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     mine = time.perf_counter() - t0
+    win1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     rank_times = gdist.all_gather_floats(mine)
     dt = max(rank_times)
 
@@ -372,6 +374,7 @@ def main():
                      "kernel_bytes_frac": gbs(k_bytes, dom_ms) / HBM_PEAK_GBS},
         "cpu_baseline": cpu,
         "detail": {"rank_seconds": rank_times, "devices": "rank r on GPU r mod %d" % torch.cuda.device_count(),
+                   "timed_window_monotonic_ns": [win0, win1],
                    "quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
                    "fm_searches_per_read": st.fm_searches / reads_per_step,
                    "quick_steps_per_read": st.quick_steps / reads_per_step,
@@ -433,6 +436,7 @@ def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_i
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    win0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     kms = qms = sms = 0.0
     for _ in range(args.steps):
         batch.run()
@@ -444,6 +448,7 @@ def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_i
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
+    win1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     rank_times = gdist.all_gather_floats(time.perf_counter() - t0)
     dt = max(rank_times)
     value = 2 * pairs * args.steps * world / dt
@@ -511,7 +516,7 @@ def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_i
                         "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                         "traffic": None, "algorithmic_bytes_per_launch": dom_ref, "avg_launch_ms": dom_ms},
            "cpu_baseline": cpu,
-           "detail": {"rank_seconds": rank_times, "quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
+           "detail": {"rank_seconds": rank_times, "timed_window_monotonic_ns": [win0, win1], "quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
                       "tier_reads": list(st.tier_reads), "tier_ms": [round(x, 3) for x in st.tier_ms],
                       "cpu_baseline_1thread": cpu1, "parity": parity, "index_build_s": t_index}}
     if rank == 0:

@@ -31,6 +31,15 @@ GWA_HD T pinv(T x) {
 #endif
   return x;
 }
+// true when c holds on any active lane of the wavefront (the lane's own c on host builds): a
+// uniform branch around work that only some lanes need
+GWA_HD bool anyLane(bool c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(c) != 0;
+#else
+  return c;
+#endif
+}
 // Region timers of the search loop (profiling builds only, -DGWA_PROF): the delta of the
 // shader clock across a region is charged once per wavefront (first active lane), so summing over
 // lanes gives wavefront cycles spent per region.
@@ -310,6 +319,20 @@ struct RefWindow {
 #pragma unroll
     for (int i = 0; i < WN; ++i) cn[i] = sn ? (rn[i] >> sn) | (rn[i + 1] << (64 - sn)) : rn[i];
   }
+  // codes (2-bit fields) and N flags of window positions [p, p + 32), -31 <= p; positions below 0
+  // read as code 0, no N
+  GWA_HD void window32(int p, uint64_t *c, uint32_t *nb) const {
+    if (p < 0) {
+      *c = c2[0] << (2 * -p);
+      *nb = (uint32_t)(cn[0] << -p);
+      return;
+    }
+    const int w = p >> 5, sh = 2 * (p & 31), wn = p >> 6, sn = p & 63;
+    const uint64_t a = pick(c2, w), b = w + 1 < W2 ? pick(c2, w + 1) : 0ULL;
+    const uint64_t an = pick(cn, wn), bn = wn + 1 < WN ? pick(cn, wn + 1) : 0ULL;
+    *c = sh ? (a >> sh) | (b << (64 - sh)) : a;
+    *nb = (uint32_t)(sn ? (an >> sn) | (bn << (64 - sn)) : an);
+  }
   // code (0-3, 4 = N) of window position j (0 <= j < 32 * W2)
   GWA_HD int code(int j) const {
     if ((pick(cn, j >> 6) >> (j & 63)) & 1) return 4;
@@ -531,6 +554,13 @@ struct BsfLane {
   }
   GWA_HD uint64_t qword(int strand, int w) const {
     return (unsigned)w < (unsigned)QW ? (uint64_t)qwL[(size_t)(strand * QW + w) * qwS] : 0ULL;
+  }
+  // 2-bit codes of strand `strand`'s read words at positions [p, p + 32); positions below 0 read as 0
+  GWA_HD uint64_t qcodes32(int strand, int p) const {
+    if (p < 0) return p <= -32 ? 0ULL : qword(strand, 0) << (2 * -p);
+    const int w = p >> 5, sh = 2 * (p & 31);
+    const uint64_t a = qword(strand, w), b = qword(strand, w + 1);
+    return sh ? (a >> sh) | (b << (64 - sh)) : a;
   }
   GWA_HD static uint64_t compressEven(uint64_t x) {
     x &= 0x5555555555555555ULL;
@@ -1219,6 +1249,7 @@ struct BsfLane {
     }
     const size_t is = (size_t)L.is;
     VpVn *hist = (VpVn *)L.chunk + L.lane;  // [col 0..N][block]: the value the reference's history holds
+    const uint64_t *h8 = (const uint64_t *)L.chunk + L.lane;  // [col 0..N]: first-tier slices
     uint64_t vp[DB], vn[DB];
     int D[DB] = {}, sb[DB];
 #pragma unroll
@@ -1240,22 +1271,23 @@ struct BsfLane {
     GWA_PT(tdf);
     // Column c of the history holds, per block, what the reference's zero-initialised arrays hold
     // after the whole pass: ~0 / 0 when the block was activated with input column c (the later
-    // write), else the value computed at column c - 1, else 0 / 0.  Column c is stored at the end
-    // of iteration c, once its activation is known, so the traceback reads one word per edit and
+    // write), else the value computed at column c - 1, else 0 / 0.  Iteration j stores column j + 1
+    // (blocks not computed at j are zeroed in their registers first: nothing reads those values,
+    // a block is re-initialised when it is activated) and, when it activates a block, rewrites
+    // that block's rows of column j to ~0 / 0.  The traceback then reads one word per edit and
     // nothing else (no per-column flags).
     // First tier (caps.dpSlice): only rows [lo, lo + 32) of column c are kept, lo = c - c0 - 17
     // around the window's middle diagonal c0 = (N - mq) / 2 (= k, the read's offset x - refStart
     // in the window, :507, away from the text ends), as one {vp 32 | vn 32} word -- 8 B per column
     // instead of 16 B per block.  A traceback that leaves the slice overflows the read into the
     // next tier, which keeps whole columns.  (dpSlice - 1 shifts the slice: tests only.)
+    // (column 0, the input column, is never read: the traceback reads columns col + 1 >= 1)
     const bool slice = caps.dpSlice != 0;
     const int c0 = ((N - mq) >> 1) + (slice ? caps.dpSlice - 1 : 0);
-    uint64_t *h8 = (uint64_t *)L.chunk + L.lane;
-    // (column 0, the input column, is never read: the traceback reads columns col + 1 >= 1)
     const size_t colStep = (size_t)bMax * is;
-    VpVn *hc = hist;
-    uint64_t *hc8 = h8;
-    uint32_t comp = 0;  // blocks computed at the previous column
+    VpVn *hc = hist;                                // column j (full columns)
+    uint64_t *hc8 = (uint64_t *)L.chunk + L.lane;   // column j (slices)
+    uint64_t lastWord = 0;                          // the slice word of column j
     uint64_t run2 = 0, runN = 0;  // the window's codes from column j on (the loop index is uniform)
     for (int j = 0; j < N; ++j) {
       if ((j & 31) == 0) run2 = pick(rw.c2, j >> 5);
@@ -1263,32 +1295,34 @@ struct BsfLane {
       const int ch = (runN & 1ULL) ? 4 : (int)(run2 & 3ULL);
       run2 >>= 2;
       runN >>= 1;
-      // every block is computed (selects, no divergent branches): blocks past bCeil give values
+      // blocks are computed with selects, not divergent branches: blocks past bCeil give values
       // nobody reads, except block bCeil, whose input is set to ~0 / 0 first -- if it is activated
-      // at this column (:427-428) its carry-in is that of the active blocks above it, as there
-      uint64_t pvp[DB], pvn[DB], x[DB];
-      int nsv[DB], hinv[DB];
-      int carry = 0;
+      // at this column (:427-428) its carry-in is that of the active blocks above it, as there.
+      // Blocks from 2 on are skipped (uniform branch) when no lane of the wavefront needs them.
+      int carry = 0, cIn = 0, nsC = 0;
+      uint64_t nextPeq = 0;
 #pragma unroll
       for (int r = 0; r < DB; ++r) {
-        pvp[r] = vp[r];
-        pvn[r] = vn[r];
-        if (r == bCeil) { vp[r] = ~0ULL; vn[r] = 0ULL; }
-        x[r] = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
-        hinv[r] = carry;
-        nsv[r] = dpBlock(x[r], carry, vp[r], vn[r]);
-        if (r < bCeil) D[r] += nsv[r];
-        carry = nsv[r];
+        int ns = 0;
+        if (r < 2 || anyLane(r <= bCeil && r < bMax)) {
+          if (r == bCeil) { vp[r] = ~0ULL; vn[r] = 0ULL; }
+          const uint64_t xr = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
+          const int hin = carry;
+          ns = dpBlock(xr, hin, vp[r], vn[r]);
+          if (r < bCeil) D[r] += ns;
+          if (r == bCeil) { cIn = hin; nsC = ns; nextPeq = xr; }  // hin = ns of block bCeil - 1
+        }
+        carry = ns;
       }
       const int bOld = bCeil;
       const int dPrev = pick(D, bCeil - 1);
-      const int cIn = pick(hinv, bCeil);  // ns of block bCeil - 1
-      const uint64_t nextPeq = pick(x, bCeil);
       const int act = bCeil < bMax && dPrev - cIn <= pick(sb, bCeil - 1) && (((nextPeq & 1ULL) != 0ULL) || cIn < 0);
       const int actBlock = act ? bCeil : -1;
 #pragma unroll
-      for (int r = 0; r < DB; ++r)
-        if (r == actBlock) D[r] = dPrev - cIn + nsv[r];
+      for (int r = 0; r < DB; ++r) {
+        if (r == actBlock) D[r] = dPrev - cIn + nsC;
+        if (!(r < bOld || r == actBlock)) { vp[r] = 0ULL; vn[r] = 0ULL; }  // not computed at j
+      }
       if (act) {
         bCeil++;
       } else {
@@ -1296,48 +1330,28 @@ struct BsfLane {
         for (int q = 0; q < DB - 1; ++q)
           if (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
       }
-      // column j: activation wins over the value computed at j - 1
-      {
-        uint64_t ev[DB], en[DB];
-#pragma unroll
-        for (int r = 0; r < DB; ++r) {
-          const bool on = r == actBlock, cp = (comp >> r) & 1u;
-          ev[r] = on ? ~0ULL : cp ? pvp[r] : 0ULL;
-          en[r] = on ? 0ULL : cp ? pvn[r] : 0ULL;
+      if (slice) {
+        if (act) {  // rows of block actBlock in column j's slice: vp 1, vn 0
+          const int lo = j - c0 - 17, r0 = 64 * actBlock - lo, r1 = r0 + 64;
+          const int s0 = r0 < 0 ? 0 : r0 > 32 ? 32 : r0, s1 = r1 < 0 ? 0 : r1 > 32 ? 32 : r1;
+          const uint64_t msk = ((s1 >= 32 ? 0xFFFFFFFFULL : (1ULL << s1) - 1ULL) & ~((1ULL << s0) - 1ULL));
+          *hc8 = (lastWord | msk) & ~(msk << 32);
         }
-        if (slice) {
-          const int lo = j - c0 - 17;
-          *hc8 = (uint64_t)rows32(ev, lo) | ((uint64_t)rows32(en, lo) << 32);
-        } else {
+        const int lo1 = j - c0 - 16;
+        lastWord = (uint64_t)rows32(vp, lo1) | ((uint64_t)rows32(vn, lo1) << 32);
+        hc8[is] = lastWord;
+      } else {
+        if (act) hc[(size_t)actBlock * is] = VpVn{~0ULL, 0ULL};
 #pragma unroll
-          for (int r = 0; r < DB; ++r)
-            if (r < bMax) hc[r * is] = VpVn{ev[r], en[r]};
-        }
+        for (int r = 0; r < DB; ++r)
+          if (r < bMax) hc[colStep + r * is] = VpVn{vp[r], vn[r]};
       }
       hc += colStep;
       hc8 += is;
-      comp = ((1u << bOld) - 1u) | (act ? 1u << bOld : 0u);
       if (bCeil == bMax) {
         const int dl = pick(D, bCeil - 1);
         if (!have) { have = 1; bestTail = j; bestDiff = dl; continue; }
         if (bestDiff > dl) { bestTail = j; bestDiff = dl; }
-      }
-    }
-    {
-      uint64_t ev[DB], en[DB];
-#pragma unroll
-      for (int r = 0; r < DB; ++r) {
-        const bool cp = (comp >> r) & 1u;
-        ev[r] = cp ? vp[r] : 0ULL;
-        en[r] = cp ? vn[r] : 0ULL;
-      }
-      if (slice) {
-        const int lo = N - c0 - 17;
-        *hc8 = (uint64_t)rows32(ev, lo) | ((uint64_t)rows32(en, lo) << 32);
-      } else {
-#pragma unroll
-        for (int r = 0; r < DB; ++r)
-          if (r < bMax) hc[r * is] = VpVn{ev[r], en[r]};
       }
     }
     GWA_PA(PR_DPF, tdf);
@@ -1380,18 +1394,30 @@ struct BsfLane {
       }
     };
     for (;;) {
-      // the run of matches: query base at row == reference base, the row's bit of Peq[ref base]
+      // the run of matches up the diagonal, 32 cells per pass: the reference codes at col - t and
+      // the query codes at row - t (t = 0..31) as 2-bit words, XOR, first nonzero field (a
+      // reference N never matches).  Query row i is read position qs + i on strand 0 and qe - 1 - i
+      // on strand 1 (dpPeq).
       int runLen = 0;
       int go = col >= 0 && row >= 0;
       while (go) {
-        const int rch = rw.code(col);
-        const int rb = row >> 6;
-        const uint64_t pq = rch == 0 ? pick(pA, rb) : rch == 1 ? pick(pC, rb) : rch == 2 ? pick(pG, rb) : pick(pT, rb);
-        const int mt = rch < 4 && ((pq >> (row & 63)) & 1ULL);
-        runLen += mt;
-        col -= mt;
-        row -= mt;
-        go = mt && col >= 0 && row >= 0;
+        uint64_t rc;
+        uint32_t rn;
+        rw.window32(col - 31, &rc, &rn);
+        rc = rev2(rc);
+        rn = rev32(rn);
+        const uint64_t qc = strand == 0 ? rev2(qcodes32(0, qs + row - 31)) : qcodes32(1, qe - 1 - row);
+        const uint64_t x = rc ^ qc;
+        const uint64_t nz = (x | (x >> 1)) & 0x5555555555555555ULL;
+        const int t1 = nz ? __builtin_ctzll(nz) >> 1 : 32;
+        const int t2 = rn ? __builtin_ctz(rn) : 32;
+        const int lim = (row < col ? row : col) + 1;
+        int t = t1 < t2 ? t1 : t2;
+        t = t < lim ? t : lim;
+        runLen += t;
+        col -= t;
+        row -= t;
+        go = t == 32 && col >= 0 && row >= 0;
       }
       if (runLen > 0) {
         leftMostPos = col + 1;

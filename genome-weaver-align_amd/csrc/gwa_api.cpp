@@ -559,6 +559,9 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
       b->maxM = (int)m;
       if (m <= 255) lens.push_back((int)m);
     }
+  if (b->maxM > 255)  // the state layout's 8-bit read positions (bsf_core.h); DESIGN.md §1
+    throw std::runtime_error("read longer than 255 bp in this batch (" + std::to_string(b->maxM) +
+                             " bp): the device path aligns reads of at most 255 bp");
   for (int m : lens) {
     int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
     b->kmax = std::max(b->kmax, k);

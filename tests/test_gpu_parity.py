@@ -140,6 +140,26 @@ def test_edge_reads(random_pair):
     _check(gi, oi, [(a, b, c if c else "I" * len(b)) for a, b, c in reads], k=2.0)
 
 
+def test_reads_longer_than_255_fail_at_batch_creation(random_pair, gwa):
+    """The device path aligns reads of at most 255 bp: a longer read fails the
+    batch before any kernel runs, with the limit in the message.  200 bp reads align as the oracle
+    does; at 224-255 bp the reference algorithm itself throws (BitVector._lshift out of bounds, the
+    oracle reproduces it) and the device path aborts the batch the same way."""
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 40, 200, 2, config_id=7)
+    strs = synth.to_strings(seqs)
+    _check(gi, oi, [(rn[i], strs[i], None) for i in range(len(strs))], k=2.0)
+    seqs, rn = synth.reads(codes, lengths, 20, 255, 2, config_id=7)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], None) for i in range(len(strs))]
+    with pytest.raises(RuntimeError, match="ArrayIndexOutOfBounds"):
+        oi.align(reads, O.OrcConfig.default(k=2.0))
+    with pytest.raises(gwa.GwaError, match="reference would abort"):
+        gwa.BidirectionalSuffixFilter(gi).align_batch(reads)
+    with pytest.raises(gwa.GwaError, match="255"):
+        gwa.BidirectionalSuffixFilter(gi).align_batch([("ok", strs[0][:100], None), ("long", strs[1] + "A", None)])
+
+
 def test_ecoli_c1_exact(gwa):
     """Config 1: E. coli-size index, 10k exact 100 bp reads (-k 0)."""
     codes, names, lengths = synth.genome(synth.ECOLI, 1)

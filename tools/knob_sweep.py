@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--k", type=float, default=2.0)
+    ap.add_argument("--c4", action="store_true", help="150 bp reads with 0-5 edits incl. indels (bench --workload c4)")
+    ap.add_argument("--strategy", default="bsf")
     ap.add_argument("--var", required=True)
     ap.add_argument("values", nargs="+")
     a = ap.parse_args()
@@ -30,8 +32,9 @@ def main():
                                                                    for i in range(4)]
         codes, names, lengths = synth.genome(contigs, config_id=1)
     gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths, device=0)
-    m = 100
-    seqs = synth.reads_codes(codes, lengths, a.reads, m, 2, config_id=2, shard=0)
+    m = 150 if a.c4 else 100
+    seqs = synth.reads_codes(codes, lengths, a.reads, m, 2, config_id=4 if a.c4 else 2, shard=0, indels=a.c4,
+                             max_edits=5)
     seq_blob = synth.SYM[seqs].tobytes()
     seq_off = np.arange(0, m * (a.reads + 1), m, dtype=np.uint64)
     name_blob, name_off = synth.name_blob(a.reads)
@@ -42,7 +45,7 @@ def main():
             os.environ.pop(a.var, None)  # "-" = unset
         else:
             os.environ[a.var] = v
-        b = gwa.Batch(gi, gwa.AlignmentConfig(k=a.k), blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
+        b = gwa.Batch(gi, gwa.AlignmentConfig(k=a.k, strategy=a.strategy), blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
         b.run()
         q = s = 0.0
         for _ in range(a.steps):

@@ -38,16 +38,44 @@ def _rows(pattern):
     return out
 
 
+def _window(d, name):
+    """bench.py's timed region (CLOCK_MONOTONIC ns, the clock of rocprofv3's timestamps) or None"""
+    f = os.path.join(d, name)
+    try:
+        with open(f) as fh:
+            w = json.loads(fh.read().strip().splitlines()[-1])["detail"]["timed_window_monotonic_ns"]
+        return int(w[0]), int(w[1])
+    except (OSError, ValueError, KeyError, IndexError):
+        return None
+
+
+def _timed_ids(d, sub, win):
+    """Dispatch ids of the align kernels that ran inside the timed window (pass `sub`)"""
+    ids = set()
+    if win is None:
+        return None
+    for r in _rows(os.path.join(d, sub, "**", "*_kernel_trace.csv")):
+        if _short(r["Kernel_Name"]) and int(r["Start_Timestamp"]) >= win[0] and int(r["End_Timestamp"]) <= win[1]:
+            ids.add(r["Dispatch_Id"])
+    return ids
+
+
 def summarise(d):
     res = {"kernels": {}}
-    # kernel trace: durations
+    # kernel trace: durations over every dispatch, and over the dispatches of bench.py's timed region
+    # (the bench line's avg_launch_ms is the mean over those; the parity, pipeline and end-to-end
+    # legs outside it launch the same kernels on other batches)
+    win = _window(d, "bench.json")
     for r in _rows(os.path.join(d, "trace", "**", "*_kernel_trace.csv")):
         k = _short(r["Kernel_Name"])
         if not k:
             continue
         e = res["kernels"].setdefault(k, {"dispatches": 0, "durations_ns": []})
         e["dispatches"] += 1
-        e["durations_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        e["durations_ns"].append(dur)
+        if win and int(r["Start_Timestamp"]) >= win[0] and int(r["End_Timestamp"]) <= win[1]:
+            e.setdefault("timed_ns", []).append(dur)
         e["vgpr"] = int(r.get("VGPR_Count") or 0)
         e["agpr"] = int(r.get("Accum_VGPR_Count") or 0)
         e["lds_bytes"] = int(r.get("LDS_Block_Size") or 0)
@@ -57,12 +85,19 @@ def summarise(d):
         e["avg_ms"] = sum(ds) / len(ds) / 1e6
         e["min_ms"] = min(ds) / 1e6
         e["max_ms"] = max(ds) / 1e6
+        t = e.pop("timed_ns", None)
+        if t:
+            e["timed_dispatches"] = len(t)
+            e["timed_avg_ms"] = sum(t) / len(t) / 1e6
     # PMC passes: average per dispatch of each counter
-    for sub in ["pmc_fetch", "pmc_sq", "pmc_tcc"]:
+    # (the PMC passes run bench.py --check 0 --no-pipeline: only the timed region's dispatches are
+    # kept when its window is known)
+    for sub, bl in [("pmc_fetch", "bench_pmc1.json"), ("pmc_sq", "bench_pmc2.json"), ("pmc_tcc", "bench_pmc3.json")]:
         acc = {}
+        keep = _timed_ids(d, sub, _window(d, bl))
         for r in _rows(os.path.join(d, sub, "**", "*_counter_collection.csv")):
             k = _short(r["Kernel_Name"])
-            if not k:
+            if not k or (keep is not None and r["Dispatch_Id"] not in keep):
                 continue
             key = (k, r["Dispatch_Id"], r["Counter_Name"])
             acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])

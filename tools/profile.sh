@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -- python3 bench.py $ARGS > $OUT/bench.json 2> $OUT/bench.err || exit $?
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d $OUT/pmc_fetch -- python3 bench.py $ARGS --no-cpu --check 0 > $OUT/bench_pmc1.json 2> $OUT/pmc1.err || exit $?
-timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace -T --output-format csv -d $OUT/pmc_sq -- python3 bench.py $ARGS --no-cpu --check 0 > $OUT/bench_pmc2.json 2> $OUT/pmc2.err || exit $?
-timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -T --output-format csv -d $OUT/pmc_tcc -- python3 bench.py $ARGS --no-cpu --check 0 > $OUT/bench_pmc3.json 2> $OUT/pmc3.err || exit $?
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d $OUT/pmc_fetch -- python3 bench.py $ARGS --no-cpu --check 0 --no-pipeline > $OUT/bench_pmc1.json 2> $OUT/pmc1.err || exit $?
+timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace -T --output-format csv -d $OUT/pmc_sq -- python3 bench.py $ARGS --no-cpu --check 0 --no-pipeline > $OUT/bench_pmc2.json 2> $OUT/pmc2.err || exit $?
+timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -T --output-format csv -d $OUT/pmc_tcc -- python3 bench.py $ARGS --no-cpu --check 0 --no-pipeline > $OUT/bench_pmc3.json 2> $OUT/pmc3.err || exit $?
 find $OUT -name "*.csv" | head -50 > $OUT/files.txt
