@@ -247,19 +247,30 @@ def main():
             f.write(rec.data)
         del rec
         t_write = time.perf_counter() - t0
-        pipe_ = gwa.Pipeline([gi], cfg)
-        with open(so, "wb") as f:
-            t0 = time.perf_counter()
-            n_e2e = pipe_.align_file(fq, f.fileno())
-            t_e2e = time.perf_counter() - t0
+        # two passes over the file on one pipeline: the first also waits for the pipeline's one-time
+        # pinning of its host buffers (started by gwa_pipeline_open), the second is the steady state
+        t0 = time.perf_counter()
+        pipe_ = gwa.Pipeline([gi], cfg)  # pins its host buffers (once per pipeline)
+        t_open = time.perf_counter() - t0
+        legs = []
+        for _ in range(2):
+            with open(so, "wb") as f:
+                t0 = time.perf_counter()
+                n_e2e = pipe_.align_file(fq, f.fileno())
+                legs.append(time.perf_counter() - t0)
+        t_e2e = legs[1]
         pst = pipe_.stats()
         pipe_.close()
         e2e = {"reads_per_s": n_e2e / t_e2e, "seconds": t_e2e, "reads": n_e2e, "fastq_bytes": os.path.getsize(fq),
+               "first_pass_reads_per_s": n_e2e / legs[0], "first_pass_seconds": legs[0], "pipeline_open_s": t_open,
                "sam_bytes": os.path.getsize(so), "fastq_write_s": t_write,
                "stages_s": {"read": pst.read_s, "frame": pst.frame_s, "setup": pst.setup_s,
                             "kernels": pst.device_kernel_s[0], "sam_format_d2h": pst.format_s, "write": pst.write_s},
-               "note": "FASTQ file -> SAM file through gwa_pipeline_align_file (1 GPU, 2 worker threads), local "
-                       "disk via the page cache; index load excluded; stage times summed over threads"}
+               "note": "FASTQ file -> SAM file through gwa_pipeline_align_file (1 GPU, 3 worker threads), local "
+                       "disk via the page cache; index load and pipeline open (pinning its read buffers, "
+                       "pipeline_open_s) excluded; reads_per_s is the second pass over the file on the same "
+                       "pipeline, first_pass_* the first (it also pins each worker's SAM buffer); stage times "
+                       "summed over threads, second pass"}
         log("end to end FASTQ -> SAM: %.0f reads/s (%d reads in %.2fs)" % (n_e2e / t_e2e, n_e2e, t_e2e))
         for x in (fq, so):
             os.remove(x)

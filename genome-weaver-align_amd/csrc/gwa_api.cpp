@@ -512,7 +512,9 @@ static bool batchHead(gwa_index *ix, const gwa_config_t *cfg, uint32_t n, gwa_ba
   sc.k = cfg->k; sc.reportType = cfg->report_type; sc.topL = cfg->top_l; sc.numSplit = cfg->num_split;
   sc.matchScore = cfg->match; sc.mismatchPenalty = cfg->mismatch; sc.splitOpenPenalty = cfg->split_open;
   sc.indelEndSkip = cfg->indel_end_skip; sc.bandWidth = cfg->band_width;
-  sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 16;
+  // 14: run a wavefront's parked reports once they are 7/8 of its live lanes (16 and 14
+  // tie on i.i.d. text; 14 is 10 % faster on the repetitive hg19r genome)
+  sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 14;
   sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
   sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
   HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
@@ -1107,6 +1109,11 @@ uint64_t batchSamInto(gwa_batch_t *b, char **buf, uint64_t *cap) {
 }
 void pinnedFree(char *p) {
   if (p) (void)hipHostFree(p);
+}
+char *pinnedAlloc(uint64_t bytes) {
+  char *p = nullptr;
+  HIPCHK(hipHostMalloc((void **)&p, bytes, hipHostMallocDefault));
+  return p;
 }
 }  // namespace gwa
 

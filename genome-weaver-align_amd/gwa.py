@@ -421,7 +421,7 @@ class Pipeline:
     """Multi-device driver (include/gwa.h gwa_pipeline_*): read batches dealt to several index replicas
     (one per GPU), SAM in input order.  indexes: FMIndexOnGenome handles, one per device."""
 
-    def __init__(self, indexes, config, batch_reads=1 << 20, workers_per_device=2):
+    def __init__(self, indexes, config, batch_reads=1 << 20, workers_per_device=0):
         self.indexes = list(indexes)
         arr = (ctypes.c_void_p * len(self.indexes))(*[ix.h.value if hasattr(ix.h, "value") else ix.h
                                                        for ix in self.indexes])

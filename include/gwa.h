@@ -187,7 +187,9 @@ int gwa_batch_read_counters(gwa_batch_t *b, int32_t *out);
  * index handles -- one per GPU, each a full replica -- and deals read batches of batch_reads reads
  * to them as they become free (workers_per_device host threads per handle overlap one batch's set-up
  * and SAM formatting with another's kernels).  Output is in input order, byte-identical to a
- * single-handle run.  The handles must outlive the pipeline. */
+ * single-handle run.  The handles must outlive the pipeline.  workers_per_device <= 0 means 3.
+ * gwa_pipeline_open pins the read-text buffers a file run keeps in flight (about 5.4 GB for one
+ * device, roughly a second); they and each worker's pinned SAM buffer are kept for later calls. */
 typedef struct gwa_pipeline gwa_pipeline_t;
 typedef struct {
   uint64_t reads, batches;

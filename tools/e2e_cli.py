@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--gz", action="store_true")
     ap.add_argument("--saved-index", action="store_true", help="run the `bwt` command first; align loads its index")
     ap.add_argument("--devices", default=None)
-    ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--workers", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20)
     a = ap.parse_args()
     import gzip
