@@ -85,6 +85,26 @@ def spawn_ranks(args):
     sys.exit(subprocess.call(cmd))
 
 
+# The chip's random-gather ceiling (tools/gather_roof.hip on MI355X, profiles/r02_gather_roof.json):
+# independent random 64-B blocks (4 x 16-B loads) and random 8-B words over a 32 GiB buffer, the
+# grid filling the chip; the rate does not change with 1-8 gathers in flight per lane.
+GATHER_BLOCK64_PER_S = 19.17e9
+GATHER_WORD8_PER_S = 47.96e9
+
+
+def gather_ceiling(st, q_ms):
+    """fm_quickscan against the random-gather roofline: the shortest time its gathers could take at
+    the measured ceilings (Occ blocks at the block rate; k-mer entries, SA values and 2 words per
+    text-mode run -- one 2-bit text line and one N-flag line -- at the word rate) over its time."""
+    words = st.kmer_lookups + st.quick_sa_reads + 2 * st.quick_text_runs
+    t_min_ms = (st.quick_blocks / GATHER_BLOCK64_PER_S + words / GATHER_WORD8_PER_S) * 1e3
+    return {"source": "profiles/r02_gather_roof.json (tools/gather_roof.hip)",
+            "note": "DRAM-miss ceiling: frac > 1 means part of the gathers hit L2 / MALL (62 % L2 hits in profiles/r02_hg19_profile.json)",
+            "block64_per_s": GATHER_BLOCK64_PER_S, "word8_per_s": GATHER_WORD8_PER_S,
+            "blocks": int(st.quick_blocks), "words": int(words), "text_runs": int(st.quick_text_runs),
+            "min_ms": t_min_ms, "avg_launch_ms": q_ms, "frac": t_min_ms / q_ms if q_ms > 0 else 0.0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -399,7 +419,8 @@ def main():
                                    "achieved_GBs": gbs(q_ref, q_ms), "frac": gbs(q_ref, q_ms) / HBM_PEAK_GBS,
                                    "kernel_bytes_per_launch": q_bytes, "kernel_bytes_GBs": gbs(q_bytes, q_ms),
                                    "kernel_bytes_frac": gbs(q_bytes, q_ms) / HBM_PEAK_GBS,
-                                   "traffic": _pmc_traffic("fm_quickscan", workload)[0]},
+                                   "traffic": _pmc_traffic("fm_quickscan", workload)[0],
+                                   "gather_ceiling": gather_ceiling(st, q_ms)},
                    "mapped": st.n_mapped, "unmapped": st.n_unmapped, "index_build_s": t_index,
                    "index_gb": gi.deviceBytes() / 1e9, "parity": parity},
     }

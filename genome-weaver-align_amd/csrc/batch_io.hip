@@ -236,6 +236,7 @@ __global__ void __launch_bounds__(256) statsKernel(const OutHeader *__restrict__
     v[11] += (unsigned)h.verifyBytes;
     v[12] += h.status == ST_MAPPED;
     v[13] += h.status == ST_UNMAPPED;
+    v[14] += (unsigned)h.quickText;
   }
   for (int f = 0; f < kStatFields; ++f) atomicAdd(&sh[f], v[f]);
   __syncthreads();

@@ -362,7 +362,7 @@ struct BsfLane {
   int nStates, heapSize, nHits, listSize, nCigar;
   int status;  // ST_*
   // instrumentation
-  int quickSteps, blocks, saReads, maxHeap, kmerLookups, shortSteps, textSteps;
+  int quickSteps, blocks, saReads, maxHeap, kmerLookups, shortSteps, textSteps, textRuns;
   int numSW, verifyBytes;  // DP verifications and their §8d bytes (instrumentation)
   // debug trace (nullptr in production launches): 4 words per event
   uint32_t *trace = nullptr;
@@ -1020,6 +1020,7 @@ struct BsfLane {
       if (uniq) {
         const int L = m - i < 32 ? m - i : 32;
         const int j = textRun(fm, tp, strand, i, L);
+        ++textRuns;
         tp = tp >= (uint64_t)j ? tp - j : tp + N - j;  // j hits, each moving to SA value tp - 1 (cyclic)
         i += j;
         quickSteps += j;
@@ -1831,6 +1832,7 @@ struct BsfLane {
     oh->kmerLookups = kmerLookups;
     oh->quickSa = saReads;
     oh->quickShort = shortSteps;
+    oh->quickText = textRuns;
   }
   // reportExactMatchAlignment (:490-494) + FMIndexOnGenome.toGenomeCoordinate (:258-269):
   // the single exact ReadHit is the reported BESTHIT/ALLHITS/TOPL result.
@@ -2190,7 +2192,7 @@ struct BsfLane {
       stairInLds = (stairLds != nullptr && m == st.ldsM) ? 1 : 0;
       stairTab = st.tab + (stairBad ? 0 : b);
     }
-    quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = textSteps = 0;
+    quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = textSteps = textRuns = 0;
     numSW = verifyBytes = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains

@@ -735,7 +735,7 @@ static const Tier kTiers[kNumTiers] = {
     // every resident lane of the chip (256 CUs x 8 waves x 64) on the next tier: the reads that
     // outgrow the LDS heap are many at k >= 4 (C4: ~57 % of 150 bp reads at k 5)
     {1024, 1024, 64, 64, 1024, 0, 128u * 1024u},
-    {4096, 4096, 256, 256, 4096, 0, 32768u},
+    {4096, 4096, 256, 256, 4096, 0, 65536u},  // 65536 lanes: C4 -m bsf tier 2 737 -> 494 ms (32768 / 131072: 737 / 601)
     {65536, 65536, 4096, 4096, 65536, 0, 1024u},
 };
 // -m sf: no quick-scan exit, every read starts with up to 2 (k + 2) seeds; heap in the slice
@@ -745,6 +745,26 @@ static const Tier kSfTiers[kNumTiers] = {
     {8192, 8192, 256, 256, 4096, 1024, 16384u},
     {65536, 65536, 4096, 4096, 65536, 16384, 1024u},
 };
+
+// lane budget of tier t: the table's, or GWA_TIER_LANES="l0,l1,l2,l3" (tuning runs)
+static uint32_t tierLanes(int t, uint32_t def) {
+  const char *e = getenv("GWA_TIER_LANES");
+  if (!e) return def;
+  for (int i = 0; i < t && e; ++i) {
+    e = strchr(e, ',');
+    if (e) ++e;
+  }
+  const long v = e ? atol(e) : 0;
+  return v > 0 ? (uint32_t)v : def;
+}
+
+// Search scratch the tiers may hold: half of what is free on the device plus what the index's
+// scratch already holds, at most 64 GiB (the index replica and the batches keep the rest).
+static uint64_t scratchBudget(const gwa_index *ix) {
+  size_t freeB = 0, totalB = 0;
+  if (hipMemGetInfo(&freeB, &totalB) != hipSuccess) return 16ull << 30;
+  return std::min<uint64_t>(64ull << 30, ((uint64_t)freeB + ix->scratchBytes) / 2);
+}
 
 // the batch's output slots + pool (gwa_layout.h OutSlots); pool counters at d_count[12..14]
 static OutSlots outSlots(const gwa_batch *b) {
@@ -841,8 +861,13 @@ int gwa_batch_run(gwa_batch_t *b) {
       caps.path = m + nref + 8;
       caps.dpSlice = t == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
       const uint64_t stride = laneBytesFor(b->R, caps);
-      uint32_t lanes = std::min<uint32_t>(n, T.maxLanes);
+      uint32_t lanes = std::min<uint32_t>(n, tierLanes(t, T.maxLanes));
       lanes = (lanes + 255) / 256 * 256;
+      {  // deep tiers: as many lanes as the scratch budget allows (at least one workgroup)
+        const uint64_t per = stride + ilvBytesFor(caps);
+        const uint64_t cap = std::max<uint64_t>(256, scratchBudget(ix) / per / 256 * 256);
+        lanes = (uint32_t)std::min<uint64_t>(lanes, cap);
+      }
       const size_t need = (size_t)(stride + ilvBytesFor(caps)) * lanes;
       if (need > ix->scratchBytes) {
         if (ix->scratch) HIPCHK(hipFree(ix->scratch));
@@ -954,6 +979,7 @@ static void ensureStats(gwa_batch *b) {
   st.states = v[9];
   st.num_sw = v[10];
   st.verify_bytes = v[11];
+  st.quick_text_runs = v[14];
   st.n_mapped = (uint32_t)v[12];
   st.n_unmapped = (uint32_t)v[13];
   b->statsDone = true;

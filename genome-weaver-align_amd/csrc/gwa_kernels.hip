@@ -247,6 +247,7 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
       h->kmerLookups = lane.kmerLookups;
       h->quickShort = lane.shortSteps;
       h->quickSa = 0;
+      h->quickText = 0;
       ovf = h->status == ST_OVERFLOW;
     }
     waveAppend(ovf, r, ovfList, ovfCount);

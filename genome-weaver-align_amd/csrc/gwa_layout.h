@@ -143,6 +143,7 @@ struct OutHeader {
   int32_t quickShort, quickSa, searchShort;  // quickSa: SA gathers of the quick scan; searchShort:
   // search FM steps answered by one text character (M_TEXT)
   int32_t verifyBytes;  // SURVEY.md §8d verify bytes: ceil(2n/8) + ceil(n/8) of each n-base window + 32 B Peq per block
+  int32_t quickText;    // text-mode runs of the quick scan (each reads one 32-base text window: textWin)
 };
 
 // Where reads write their reported hits: read r owns the fixed slot hits[r * hitCap, + hitCap) and

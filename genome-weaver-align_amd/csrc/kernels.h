@@ -27,7 +27,7 @@ void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream
 // batch_io.hip: reads in (encode on the device), SAM out (two-pass formatting), batch statistics
 struct SamText;
 constexpr uint32_t kLenSeen = 65536;  // read-length presence table (lengths >= 65535 share the last slot)
-constexpr int kStatFields = 14;
+constexpr int kStatFields = 15;
 void launchEncode(const char *seq, const uint64_t *seqB, const uint64_t *seqE, uint32_t n, uint32_t *codeLen,
                   uint32_t *rowLen, uint32_t *codeOff, uint32_t *lenSeen, uint8_t *codes, void *scanTmp,
                   size_t scanTmpBytes, int pass, hipStream_t s);

@@ -55,7 +55,8 @@ class BatchStats(ctypes.Structure):
                 ("n_mapped", ctypes.c_uint32), ("n_unmapped", ctypes.c_uint32), ("kmer_lookups", ctypes.c_uint64),
                 ("quick_short_steps", ctypes.c_uint64), ("quick_sa_reads", ctypes.c_uint64),
                 ("search_short_steps", ctypes.c_uint64), ("tier_ms", ctypes.c_float * 4),
-                ("num_sw", ctypes.c_uint64), ("verify_bytes", ctypes.c_uint64)]
+                ("num_sw", ctypes.c_uint64), ("verify_bytes", ctypes.c_uint64),
+                ("quick_text_runs", ctypes.c_uint64)]
 
 
 class PipelineStats(ctypes.Structure):

@@ -107,6 +107,7 @@ typedef struct {
   float tier_ms[4];        /* search time per capacity tier (HIP events) */
   uint64_t num_sw;         /* DP verifications (alignBlockDetailed calls) */
   uint64_t verify_bytes;   /* SURVEY.md 8(d) bytes of those verifications (reference window + Peq) */
+  uint64_t quick_text_runs; /* fm_quickscan text-mode runs (one 32-base 2-bit text window + N flags each) */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);

@@ -48,15 +48,19 @@ def main():
         b = gwa.Batch(gi, gwa.AlignmentConfig(k=a.k, strategy=a.strategy), blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
         b.run()
         q = s = 0.0
+        tms = [0.0] * 4
         for _ in range(a.steps):
             b.run()
             st = b.stats()
             q += st.quickscan_ms
             s += st.search_ms
+            tms = [x + y for x, y in zip(tms, st.tier_ms)]
         sam, _ = b.results(0, 2000)
         same = ref is None or sam == ref
         ref = ref or sam
-        print("%s=%s quickscan_ms=%.2f search_ms=%.2f same_sam=%s" % (a.var, v, q / a.steps, s / a.steps, same), flush=True)
+        print("%s=%s quickscan_ms=%.2f search_ms=%.2f tier_ms=%s tier_reads=%s same_sam=%s"
+              % (a.var, v, q / a.steps, s / a.steps, [round(x / a.steps, 1) for x in tms], list(st.tier_reads), same),
+              flush=True)
         b.close()
 
 
