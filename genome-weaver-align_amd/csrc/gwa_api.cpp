@@ -746,9 +746,9 @@ static const Tier kSfTiers[kNumTiers] = {
     {65536, 65536, 4096, 4096, 65536, 16384, 1024u},
 };
 
-// lane budget of tier t: the table's, or GWA_TIER_LANES="l0,l1,l2,l3" (tuning runs)
-static uint32_t tierLanes(int t, uint32_t def) {
-  const char *e = getenv("GWA_TIER_LANES");
+// value t of a comma-separated tuning list in env variable `var`, or def
+static uint32_t tierValue(const char *var, int t, uint32_t def) {
+  const char *e = getenv(var);
   if (!e) return def;
   for (int i = 0; i < t && e; ++i) {
     e = strchr(e, ',');
@@ -854,6 +854,12 @@ int gwa_batch_run(gwa_batch_t *b) {
       const Tier &T = sf ? kSfTiers[t] : kTiers[t];
       Caps caps;
       caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
+      if (t > 0 && !sf) {  // GWA_TIER_ARENA="a0,a1,a2,a3": arena / heap states of tiers >= 1 (tuning runs)
+        const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", t, (uint32_t)T.arena), 65536u);
+        caps.arena = caps.heap = a;
+        caps.hits = caps.list = (int)tierValue("GWA_TIER_HITS", t, (uint32_t)T.hits);  // hit list / report list
+        caps.cigar = (int)tierValue("GWA_TIER_CIGAR", t, (uint32_t)T.cigar);
+      }
       caps.cand = T.cand;
       const int bMax = std::max(1, (m + 63) / 64);
       const int nref = m + 2 * b->kmax + 2;
@@ -861,7 +867,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       caps.path = m + nref + 8;
       caps.dpSlice = t == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
       const uint64_t stride = laneBytesFor(b->R, caps);
-      uint32_t lanes = std::min<uint32_t>(n, tierLanes(t, T.maxLanes));
+      uint32_t lanes = std::min<uint32_t>(n, tierValue("GWA_TIER_LANES", t, T.maxLanes));
       lanes = (lanes + 255) / 256 * 256;
       {  // deep tiers: as many lanes as the scratch budget allows (at least one workgroup)
         const uint64_t per = stride + ilvBytesFor(caps);

@@ -4,5 +4,5 @@ set -o pipefail
 TAG=${1:-tiers}
 cd "${GRAFT_REPO_ROOT:-$(dirname $0)/..}"
 mkdir -p gpurun_out
-timeout -k 10 500 python -u tools/knob_sweep.py --genome hg19 --c4 --k 5 --reads 1000000 --steps 1 --var GWA_TIER_LANES - 0,0,65536,0 0,0,131072,0 0,0,131072,4096 0,262144,131072,4096 > gpurun_out/${TAG}_c4.log 2>&1 || { tail -20 gpurun_out/${TAG}_c4.log; exit 1; }
+timeout -k 10 500 python -u tools/knob_sweep.py --genome hg19 --c4 --k 5 --reads 1000000 --steps 1 --var GWA_TIER_HITS - 0,256,0,0 0,256,1024,0 0,1024,4096,0 > gpurun_out/${TAG}_c4.log 2>&1 || { tail -20 gpurun_out/${TAG}_c4.log; exit 1; }
 cat gpurun_out/${TAG}_c4.log
