@@ -53,6 +53,48 @@ __global__ void __launch_bounds__(256) g_block64(const u32x4 *buf, uint64_t nblo
   if (acc == 0x12345678u) out[0] = (uint32_t)g;
 }
 
+// The same random 64-B blocks, loaded cooperatively by the 4 lanes of a quad: for each of the
+// quad's 4 blocks in turn, lane q of the quad loads bytes [16q, 16q + 16) of it, so one load
+// instruction covers 16 whole blocks (one 64-B line each) instead of 64 quarter blocks.  The owner
+// gets its block back through 12 quad permutes (__shfl within the quad).
+template <int D>
+__global__ void __launch_bounds__(256) g_block64_quad(const u32x4 *buf, uint64_t nblocks, int rounds, uint32_t *out) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = (int)(threadIdx.x & 63), q = lane & 3, qb = lane & ~3;
+  uint64_t st[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) st[d] = mix(g * D + d);
+  uint32_t acc = 0;
+  for (int r = 0; r < rounds; ++r) {
+    u32x4 v[D][4];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const uint64_t mine = (st[d] >> 20) & (nblocks - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t bj = (uint64_t)__shfl((long long)mine, qb + j);
+        v[d][j] = __builtin_nontemporal_load(buf + bj * 4 + q);  // part q of block j
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      // owner q needs part p of its block from lane qb + p, which holds it in v[d][q]
+      uint32_t x = 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        u32x4 w = v[d][0];
+#pragma unroll
+        for (int j = 1; j < 4; ++j) w = ((lane & 3) == j) ? v[d][j] : w;  // what this lane sends: v[q'] for owner q'...
+        const uint32_t y = (uint32_t)__shfl((int)(p == 0 ? w.x : p == 1 ? w.y : p == 2 ? w.z : w.w), qb + p);
+        x ^= y;
+      }
+      acc += x;
+      st[d] = st[d] * 6364136223846793005ULL + (1442695040888963407ULL ^ x);
+    }
+  }
+  if (acc == 0x12345678u) out[0] = (uint32_t)g;
+}
+
 // D random 8-B words per lane per round (k-mer entries, text words)
 template <int D>
 __global__ void __launch_bounds__(256) g_word8(const uint64_t *buf, uint64_t nwords, int rounds, uint32_t *out) {
@@ -125,6 +167,8 @@ int main() {
   RUN("block64", 1, hipLaunchKernelGGL(g_block64<1>, grid, blk, 0, 0, (const u32x4 *)buf, bytes / 64, rounds, out), 64.0)
   RUN("block64", 2, hipLaunchKernelGGL(g_block64<2>, grid, blk, 0, 0, (const u32x4 *)buf, bytes / 64, rounds, out), 64.0)
   RUN("block64", 4, hipLaunchKernelGGL(g_block64<4>, grid, blk, 0, 0, (const u32x4 *)buf, bytes / 64, rounds, out), 64.0)
+  RUN("block64quad", 1, hipLaunchKernelGGL(g_block64_quad<1>, grid, blk, 0, 0, (const u32x4 *)buf, bytes / 64, rounds, out), 64.0)
+  RUN("block64quad", 2, hipLaunchKernelGGL(g_block64_quad<2>, grid, blk, 0, 0, (const u32x4 *)buf, bytes / 64, rounds, out), 64.0)
   RUN("word8", 1, hipLaunchKernelGGL(g_word8<1>, grid, blk, 0, 0, (const uint64_t *)buf, bytes / 8, rounds, out), 64.0)
   RUN("word8", 2, hipLaunchKernelGGL(g_word8<2>, grid, blk, 0, 0, (const uint64_t *)buf, bytes / 8, rounds, out), 64.0)
   RUN("word8", 4, hipLaunchKernelGGL(g_word8<4>, grid, blk, 0, 0, (const uint64_t *)buf, bytes / 8, rounds, out), 64.0)
