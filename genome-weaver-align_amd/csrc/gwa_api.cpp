@@ -225,6 +225,11 @@ static void buildFromDeviceText(gwa_index *ix, uint8_t *dT) {
   for (int c = 0; c < 5; ++c) v.C[c] = h.C[c];
   // k-mer interval tables for FMQuickScan restarts (IndexView::kmer)
   v.kmerK = kmerKFor(N);
+  if (const char *e = getenv("GWA_KMER_K")) {  // tuning runs: a larger table, up to log4(N) and 16
+    int l = 0;
+    while (l < 31 && (1ULL << (2 * (l + 1))) <= N) ++l;
+    v.kmerK = std::max(0, std::min({atoi(e), l, 16}));
+  }
   if (v.kmerK > 0) {
     const uint64_t nk = 1ULL << (2 * v.kmerK);
     for (int f = 0; f < 2; ++f) {
