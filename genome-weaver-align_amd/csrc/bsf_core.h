@@ -197,6 +197,7 @@ struct Caps {
   int32_t arena, heap, hits, list, cigar, dpWords, path;
   int32_t dpSlice;  // 1: the DP history keeps a 32-row slice around the read's diagonal (first tier)
   int32_t cand;  // SuffixFilter candidate set (sf_core.h); 0 on the BSF path
+  int32_t sparse;  // > 1: only every sparse-th lane of a wavefront takes reads (deep tiers, bsf_search_kernel)
 };
 
 // Per-lane scratch.  The search structures (arena/heap/hits/list/cigar) sit in a per-lane slice;

@@ -858,6 +858,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     while (n > 0) {
       const Tier &T = sf ? kSfTiers[t] : kTiers[t];
       Caps caps;
+      caps.sparse = 0;
       caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
       if (t > 0 && !sf) {  // GWA_TIER_ARENA="a0,a1,a2,a3": arena / heap states of tiers >= 1 (tuning runs)
         const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", t, (uint32_t)T.arena), 65536u);
@@ -878,6 +879,20 @@ int gwa_batch_run(gwa_batch_t *b) {
         const uint64_t per = stride + ilvBytesFor(caps);
         const uint64_t cap = std::max<uint64_t>(256, scratchBudget(ix) / per / 256 * 256);
         lanes = (uint32_t)std::min<uint64_t>(lanes, cap);
+      }
+      if (t > 0 && !sf) {
+        // a deep tier with few reads: 64 / s reads per wavefront (every s-th lane), the largest s
+        // whose n x s lanes stay within GWA_SPARSE_LANES (default 262144) and the scratch budget
+        const uint64_t per = stride + ilvBytesFor(caps), maxSparse = tierValue("GWA_SPARSE_LANES", 0, 262144u);
+        const uint64_t budget = scratchBudget(ix);
+        for (uint32_t s = 64; s >= 2; s /= 2) {
+          const uint64_t sl = ((uint64_t)n * s + 255) / 256 * 256;
+          if (sl <= maxSparse && sl * per <= budget) {
+            lanes = (uint32_t)sl;
+            caps.sparse = (int32_t)s;
+            break;
+          }
+        }
       }
       const size_t need = (size_t)(stride + ilvBytesFor(caps)) * lanes;
       if (need > ix->scratchBytes) {

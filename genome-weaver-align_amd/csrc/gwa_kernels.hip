@@ -142,6 +142,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED };
   int phase = IDLE;
   uint32_t r = 0;
+  // deep tiers with few reads (caps.sparse > 1): only every caps.sparse-th lane takes reads, so the
+  // long searches of a tier spread over more wavefronts instead of diverging inside few
+  if (caps.sparse > 1 && ((gid & 63) % (uint32_t)caps.sparse) != 0) phase = EXHAUSTED;
   for (;;) {
     const bool need = phase == IDLE;
     const uint64_t needMask = __ballot(need);
