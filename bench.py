@@ -1,8 +1,12 @@
 """bench.py -- reads/s of the MI355X `align -m bsf` path (BASELINE.json metric).
 
-One step = one pass of the hot path (fm_quickscan + bsf_search tiers) over one batch of synthetic
-100 bp reads already resident in HBM.  Weak scaling: every rank holds a full index replica on its
-own GPU and aligns its own shard; value = total reads of all ranks / max-over-ranks time.
+One step = the whole device path over one batch of synthetic 100 bp reads whose text is already
+resident in HBM: encode the read text (gwa_batch_run starts from it, as the reference's per-read
+call starts from the Read's String), fm_quickscan + bsf_search tiers, and the SAM text of every read
+written in HBM (gwa_batch_format; A/Align.java:187-195 -> A/SAMOutput.java:73-82).  Weak scaling:
+every rank holds a full index replica on its own GPU and aligns its own shard; value = total reads
+of all ranks / max-over-ranks time.  At N = 1 the default run adds detail.hg19r, the same step on the
+hg19-like repetitive genome.
 
   python bench.py [--gpus N --steps K --warmup W] [--genome hg19|hg19r|ecoli|<Mbp>] [--reads R]
 
@@ -105,32 +109,150 @@ def gather_ceiling(st, q_ms):
             "min_ms": t_min_ms, "avg_launch_ms": q_ms, "frac": t_min_ms / q_ms if q_ms > 0 else 0.0}
 
 
+def median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2]
+
+
+def cpu_baselines(oi, read_tuple, n_avail, strategy, k, args, O, label):
+    """The oracle (C++ restatement of the reference path) on this host, each leg the median of 3
+    runs: (i) 1 thread, as the reference runs (A/Align.java:174-196); (ii) every core this process
+    may use, contiguous read ranges.  -> (cpu_baseline, cpu_baseline_1thread)."""
+    T, tdesc = host_cores()
+    if args.cpu_threads:
+        T = args.cpu_threads
+    model = cpu_model()
+    ocfg = O.OrcConfig.default(k=k, strategy=strategy)
+    ns = min(args.cpu_sample, n_avail)
+    r1 = [read_tuple(i) for i in range(ns)]
+    runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        oi.align(r1, ocfg)
+        runs.append(time.perf_counter() - t0)
+    ct = median(runs)
+    cpu1 = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port", "seconds": ct,
+            "runs_s": runs, "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the "
+                                     "reference %s path (oracle/; CPU restatement, not the JVM), same index; median "
+                                     "of 3 runs; %s" % (ns, label, model)}
+    log("cpu baseline (1 thread): %.0f reads/s (%d reads, median of %s s)" % (ns / ct, ns, ["%.2f" % x for x in runs]))
+    cpu = cpu1
+    if T > 1:
+        nt = int(min(n_avail, max(ns, args.cpu_seconds * cpu1["value"] * T)))
+        rt = r1 + [read_tuple(i) for i in range(ns, nt)]
+        runs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            oi.align(rt, ocfg, threads=T)
+            runs.append(time.perf_counter() - t0)
+        ct = median(runs)
+        cpu = {"value": nt / ct, "unit": "reads/s", "cores": T, "kind": "port", "seconds": ct, "runs_s": runs,
+               "sample": "first %d reads of rank 0's batch on %d host threads (%s; contiguous ranges, one Aligner "
+                         "each), C++ restatement of the reference %s path (oracle/; CPU restatement, not the JVM), "
+                         "same index; median of 3 runs; %s" % (nt, T, tdesc, label, model)}
+        log("cpu baseline (%d threads): %.0f reads/s (%d reads, median of %s s)"
+            % (T, nt / ct, nt, ["%.2f" % x for x in runs]))
+    return cpu, cpu1
+
+
+def timed_steps(batch, steps, warmup, barrier):
+    """W untimed and K timed steps of the whole device path (gwa_batch_run = encode + fm_quickscan +
+    search tiers, then gwa_batch_format = SAM text in HBM), bracketed by barrier + synchronize.
+    -> (this rank's seconds, window, per-kernel ms sums, last stats)"""
+    import torch
+    for _ in range(warmup):
+        batch.run()
+        batch.format_device()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    win0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # the rocprofv3 trace's clock (tools/prof_summary.py)
+    acc = dict(encode=0.0, quickscan=0.0, search=0.0, format=0.0, kernel=0.0)
+    sam_bytes = 0
+    st = None
+    for _ in range(steps):
+        batch.run()
+        sam_bytes = batch.format_device()
+        st = batch.stats()
+        acc["encode"] += st.encode_ms
+        acc["quickscan"] += st.quickscan_ms
+        acc["search"] += st.search_ms
+        acc["format"] += st.format_ms
+        acc["kernel"] += st.kernel_ms
+    torch.cuda.synchronize()
+    barrier()
+    mine = time.perf_counter() - t0
+    win1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+    return mine, [win0, win1], {k: v / max(1, steps) for k, v in acc.items()}, st, sam_bytes
+
+
+def make_reads(synth, np, codes, lengths, n, m, c4, rank):
+    """Synthetic reads: C2 100 bp with 0-2 substitutions; C4 150 bp with 0-5 edits,
+    60 % substitutions / 20 % 1-bp insertions / 20 % 1-bp deletions; shard = rank."""
+    seqs = synth.reads_codes(codes, lengths, n, m, 2, config_id=4 if c4 else 2, shard=rank, indels=c4, max_edits=5)
+    seq_blob = synth.SYM[seqs].tobytes()
+    del seqs
+    seq_off = np.arange(0, m * (n + 1), m, dtype=np.uint64)
+    name_blob, name_off = synth.name_blob(n)
+    qual_blob = b"I" * (m * n)
+    return (name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off)
+
+
+def hg19r_leg(args, gen, gwa, synth, np, cfg, log):
+    """detail.hg19r: the same C2 step on the hg19-like repetitive genome (tools/synth.genome_repeats,
+    generated by a child process while the main leg ran)."""
+    import torch
+    gen_proc, path = gen
+    t0 = time.time()
+    if gen_proc.wait() != 0:
+        raise SystemExit("hg19r genome generation failed")
+    codes = np.load(path)
+    os.remove(path)
+    names = [c[0] for c in synth.HG19_CONTIGS]
+    lengths = [c[1] for c in synth.HG19_CONTIGS]
+    gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths, device=torch.cuda.current_device())
+    n = args.reads or 10_000_000
+    blobs = make_reads(synth, np, codes, lengths, n, 100, False, 0)
+    del codes
+    batch = gwa.Batch(gi, cfg, blobs=blobs)
+    dt, _, kms, st, _ = timed_steps(batch, 2, 1, lambda: None)
+    out = {"value": 2 * n / dt, "unit": "reads/s", "ms_per_step": dt * 1e3 / 2, "steps": 2, "warmup": 1,
+           "reads_per_step": n, "kernels_ms": kms, "tier_reads": list(st.tier_reads),
+           "tier_ms": [round(x, 3) for x in st.tier_ms],
+           "genome": "hg19-like synthetic (hg19 contig lengths, N gaps, interspersed repeat families, satellites, "
+                     "segmental duplications; tools/synth.genome_repeats)", "leg_s": time.time() - t0}
+    log("hg19r leg: %.0f reads/s (%.1f ms per step; tiers %s)" % (out["value"], out["ms_per_step"], out["tier_reads"]))
+    batch.close()
+    gi.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--genome", default=os.environ.get("GWA_BENCH_GENOME", "hg19"),
-                    help="hg19: hg19 contig lengths, i.i.d. ACGT (the BASELINE config); hg19r: hg19-like "
-                         "repeats and N gaps (tools/synth.genome_repeats); ecoli; or a size in Mbp")
+                    help="hg19: hg19 contig lengths, i.i.d. ACGT with hg19-like N-gap runs (the BASELINE stand-in, "
+                         "SURVEY.md 8(d)); hg19r: hg19-like repeats and N gaps (tools/synth.genome_repeats); ecoli; "
+                         "or a size in Mbp")
     ap.add_argument("--reads", type=int, default=int(os.environ.get("GWA_BENCH_READS", "0")))
     ap.add_argument("--k", type=float, default=None, help="max edits (default: 2 for c2, 5 for c4)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
                     help="c2: 100 bp, 0-2 substitutions (the BASELINE metric); c4: 150 bp, 0-5 edits with indels; "
                          "c5: 2x100 bp paired-end, insert ~ N(300, 30), proper pairs within [210, 390]")
     ap.add_argument("--strategy", default="bsf", choices=["bsf", "sf"], help="-m (align strategy)")
-    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "100000")),
-                    help="reads of the single-thread CPU baseline (SURVEY.md 8(d)(i))")
+    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("GWA_CPU_SAMPLE", "40000")),
+                    help="reads of the single-thread CPU baseline (SURVEY.md 8(d)(i)), each of 3 runs")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the multi-core CPU baseline (default: the cores this process may use)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target duration of the multi-core CPU baseline (sample sized from the 1-thread rate)")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0,
+                    help="target duration of each of the 3 multi-core CPU baseline runs (sample sized from the 1-thread rate)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=20000,
                     help="random reads of step 0 checked against the oracle (plus every read a search tier >= 1 ran)")
-    ap.add_argument("--sa-check", type=int, default=1 << 20,
-                    help="adjacent suffix-array pairs checked independently (plus a permutation check)")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the host-pipeline (FASTQ-to-SAM) leg")
+    ap.add_argument("--no-hg19r", action="store_true", help="skip the detail.hg19r leg (default C2 run at N=1 only)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -138,14 +260,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    c4 = args.workload == "c4"
+    # the hg19r leg's genome is generated by a child process (started before this process touches
+    # the GPU) while the main leg runs
+    gen = None
+    if (world == 1 and args.workload == "c2" and args.genome == "hg19" and not args.no_hg19r and args.strategy == "bsf"
+            and args.k in (None, 2.0)):
+        import subprocess
+        import tempfile
+        import shutil
+        d = "/dev/shm" if os.path.isdir("/dev/shm") and shutil.disk_usage("/dev/shm").free > (8 << 30) else tempfile.gettempdir()
+        path = os.path.join(d, "gwa_bench_hg19r_%d.npy" % os.getpid())
+        gen = (subprocess.Popen([sys.executable, os.path.join(REPO, "tools", "synth.py"), "hg19r", path]), path)
 
     import numpy as np
     import synth
     import gwa
     import dist as gdist
 
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -157,8 +291,8 @@ def main():
     t0 = time.time()
     if args.genome in ("hg19", "hg19r"):
         if args.genome == "hg19":
-            codes, names, lengths = synth.genome(synth.HG19_CONTIGS, config_id=1)
-            gname = "hg19-size synthetic (i.i.d. ACGT, hg19 contig lengths)"
+            codes, names, lengths = synth.genome_ngaps(synth.HG19_CONTIGS, config_id=1)
+            gname = "hg19-size synthetic (hg19 contig lengths, i.i.d. ACGT, hg19-like N-gap runs)"
         else:
             codes, names, lengths = synth.genome_repeats(synth.HG19_CONTIGS, config_id=1)
             gname = ("hg19-like synthetic (hg19 contig lengths, N gaps, interspersed repeat families, satellites, "
@@ -170,7 +304,6 @@ def main():
         mb = float(args.genome)
         codes, names, lengths = synth.genome([("chr%d" % (i + 1), int(mb * 1e6 / 4)) for i in range(4)], config_id=1)
         gname = "%g Mbp synthetic (4 contigs, i.i.d. ACGT)" % mb
-    c4 = args.workload == "c4"
     if args.k is None:
         args.k = 5.0 if c4 else 2.0
     reads_per_step = args.reads or (1_000_000 if c4 else 10_000_000 if args.genome.startswith("hg19") else 1_000_000)
@@ -178,62 +311,39 @@ def main():
     t0 = time.time()
     gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths, device=dev)
     t_index = time.time() - t0
-    log("index built + resident in HBM: %.1fs, %.2f GB" % (t_index, gi.deviceBytes() / 1e9))
+    index_gb = gi.deviceBytes() / 1e9
+    log("index built + resident in HBM: %.1fs, %.2f GB" % (t_index, index_gb))
 
     cfg = gwa.AlignmentConfig(k=args.k, strategy=args.strategy)
     if args.workload == "c5":
         return bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_index)
-    # synthetic reads: C2 100 bp with 0-2 substitutions; C4 150 bp with 0-5 edits,
-    # 60 % substitutions / 20 % 1-bp insertions / 20 % 1-bp deletions; shard = rank
     m = 150 if c4 else 100
     t0 = time.time()
-    seqs = synth.reads_codes(codes, lengths, reads_per_step, m, 2, config_id=4 if c4 else 2, shard=rank,
-                             indels=c4, max_edits=5)
-    seq_blob = synth.SYM[seqs].tobytes()
-    del seqs
-    seq_off = np.arange(0, m * (reads_per_step + 1), m, dtype=np.uint64)
-    name_blob, name_off = synth.name_blob(reads_per_step)
-    qual_blob = b"I" * (m * reads_per_step)
+    blobs = make_reads(synth, np, codes, lengths, reads_per_step, m, c4, rank)
+    name_blob, name_off, seq_blob, seq_off, qual_blob, _ = blobs
     log("reads generated in %.1fs" % (time.time() - t0))
     t0 = time.time()
-    batch = gwa.Batch(gi, cfg, blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
+    batch = gwa.Batch(gi, cfg, blobs=blobs)
     log("batch resident in HBM: %.1fs" % (time.time() - t0))
 
     def read_tuple(i):
         return (name_blob[10 * i:10 * i + 10].decode(), seq_blob[m * i:m * i + m].decode(), "I" * m)
 
-    for _ in range(args.warmup):
-        batch.run()
-
     def barrier():
         if dist:
             tdist.barrier()
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    win0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # the rocprofv3 trace's clock (tools/prof_summary.py)
-    kms = qms = sms = 0.0
-    for _ in range(args.steps):
-        batch.run()
-        st = batch.stats()
-        kms += st.kernel_ms
-        qms += st.quickscan_ms
-        sms += st.search_ms
-    torch.cuda.synchronize()
-    barrier()
-    mine = time.perf_counter() - t0
-    win1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+    mine, window, kms, st, sam_bytes = timed_steps(batch, args.steps, args.warmup, barrier)
     rank_times = gdist.all_gather_floats(mine)
     dt = max(rank_times)
 
     # host pipeline (first bullet): the whole path for one batch outside the timed
-    # region -- reads from host memory to HBM (batch create), kernels, records back to the host and SAM
-    # text -- reported beside `value`, never as it
+    # region -- reads from host memory to HBM (batch create), kernels, SAM text to the host -- reported
+    # beside `value`, never as it
     pipe = None
     if rank == 0 and not args.no_pipeline:
         t0 = time.perf_counter()
-        b2 = gwa.Batch(gi, cfg, blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
+        b2 = gwa.Batch(gi, cfg, blobs=blobs)
         t1 = time.perf_counter()
         b2.run()
         t2 = time.perf_counter()
@@ -267,10 +377,10 @@ def main():
             f.write(rec.data)
         del rec
         t_write = time.perf_counter() - t0
-        # two passes over the file on one pipeline: the first also waits for the pipeline's one-time
-        # pinning of its host buffers (started by gwa_pipeline_open), the second is the steady state
+        # two passes over the file on one pipeline: the first also pins the pipeline's host buffers,
+        # the second is the steady state
         t0 = time.perf_counter()
-        pipe_ = gwa.Pipeline([gi], cfg)  # pins its host buffers (once per pipeline)
+        pipe_ = gwa.Pipeline([gi], cfg)
         t_open = time.perf_counter() - t0
         legs = []
         for _ in range(2):
@@ -287,10 +397,9 @@ def main():
                "stages_s": {"read": pst.read_s, "frame": pst.frame_s, "setup": pst.setup_s,
                             "kernels": pst.device_kernel_s[0], "sam_format_d2h": pst.format_s, "write": pst.write_s},
                "note": "FASTQ file -> SAM file through gwa_pipeline_align_file (1 GPU, 3 worker threads), local "
-                       "disk via the page cache; index load and pipeline open (pinning its read buffers, "
-                       "pipeline_open_s) excluded; reads_per_s is the second pass over the file on the same "
-                       "pipeline, first_pass_* the first (it also pins each worker's SAM buffer); stage times "
-                       "summed over threads, second pass"}
+                       "disk via the page cache; index load and pipeline open excluded; reads_per_s is the second "
+                       "pass over the file on the same pipeline, first_pass_* the first (it also pins the host "
+                       "buffers); stage times summed over threads, second pass"}
         log("end to end FASTQ -> SAM: %.0f reads/s (%d reads in %.2fs)" % (n_e2e / t_e2e, n_e2e, t_e2e))
         for x in (fq, so):
             os.remove(x)
@@ -303,8 +412,8 @@ def main():
     deep = np.nonzero(counters[:, 12] >= 1)[0]
 
     # parity (checker only): a random sample of this rank's reads plus every read a search tier >= 1
-    # ran, GPU SAM against the oracle.  The oracle index takes the GPU suffix arrays only after an
-    # independent check of them (permutation + sampled adjacent-rotation order, oracle C++).
+    # ran, GPU SAM against the oracle.  The oracle index takes the GPU suffix arrays only after a
+    # complete independent check of them (permutation + every adjacent pair, oracle C++).
     parity = None
     oi = None
     if rank == 0 and (args.check or (not args.no_cpu and args.cpu_sample > 0)):
@@ -312,11 +421,10 @@ def main():
         import oracle as O
         t0 = time.time()
         sa_f, sa_r = gi.suffixArray(0), gi.suffixArray(1)
-        O.check_cyclic_sa(codes, sa_f, samples=args.sa_check, seed=11, threads=host_cores()[0])
-        O.check_cyclic_sa(np.ascontiguousarray(codes[::-1]), sa_r, samples=args.sa_check, seed=12,
-                          threads=host_cores()[0])
+        O.check_cyclic_sa_full(codes, sa_f, threads=host_cores()[0])
+        O.check_cyclic_sa_full(np.ascontiguousarray(codes[::-1]), sa_r, threads=host_cores()[0])
         t_sa = time.time() - t0
-        log("GPU suffix arrays pass the independent check (%d sampled pairs per strand): %.1fs" % (args.sa_check, t_sa))
+        log("GPU suffix arrays pass the complete check (every adjacent pair, both strands): %.1fs" % t_sa)
         oi = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
         del sa_f, sa_r
         t_oidx = time.time() - t0 - t_sa
@@ -329,51 +437,23 @@ def main():
         exp = oi.align(sreads, O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy]),
                        threads=host_cores()[0])
         parity = {"reads": int(len(samp)), "random": int(min(args.check, reads_per_step)), "tier_ge1": int(len(deep)),
-                  "identical": got == exp, "sa_check_pairs": args.sa_check,
+                  "identical": got == exp, "sa_check": "complete (every adjacent pair, both strands)",
                   "note": "random reads + every read of search tiers >= 1; oracle index from the GPU suffix arrays "
-                          "after an independent permutation + adjacent-order check"}
+                          "after a complete independent permutation + adjacent-order check"}
         log("parity on %d reads (%d from tiers >= 1): %s (oracle index %.1fs)" % (len(samp), len(deep), got == exp, t_oidx))
 
-    # CPU baseline: the oracle (C++ restatement of the reference path) on this host.
-    # (i) 1 thread, as the reference runs (A/Align.java:174-196); (ii) every core this process may use,
-    # contiguous read ranges.  cpu_baseline reports (ii); (i) is kept in detail.
     cpu = cpu1 = None
     if rank == 0 and not args.no_cpu and args.cpu_sample > 0:
-        T, tdesc = host_cores()
-        if args.cpu_threads:
-            T = args.cpu_threads
-        model = cpu_model()
-        ocfg = O.OrcConfig.default(k=args.k, strategy=gwa.STRATEGIES[args.strategy])
-        ns = min(args.cpu_sample, reads_per_step)
-        r1 = [read_tuple(i) for i in range(ns)]
-        t0 = time.perf_counter()
-        oi.align(r1, ocfg)
-        ct = time.perf_counter() - t0
-        cpu1 = {"value": ns / ct, "unit": "reads/s", "cores": 1, "kind": "port", "seconds": ct,
-                "sample": "first %d reads of rank 0's batch, single-thread C++ restatement of the reference "
-                          "%s path (oracle/; CPU restatement, not the JVM), same index; %s"
-                          % (ns, args.strategy.upper(), model)}
-        log("cpu baseline (1 thread): %.0f reads/s (%d reads in %.1fs)" % (ns / ct, ns, ct))
-        cpu = cpu1
-        if T > 1:
-            nt = int(min(reads_per_step, max(ns, args.cpu_seconds * cpu1["value"] * T)))
-            rt = r1 + [read_tuple(i) for i in range(ns, nt)]
-            t0 = time.perf_counter()
-            oi.align(rt, ocfg, threads=T)
-            ct = time.perf_counter() - t0
-            cpu = {"value": nt / ct, "unit": "reads/s", "cores": T, "kind": "port", "seconds": ct,
-                   "sample": "first %d reads of rank 0's batch on %d host threads (%s; contiguous ranges, one "
-                             "Aligner each), C++ restatement of the reference %s path (oracle/; CPU restatement, "
-                             "not the JVM), same index; %s" % (nt, T, tdesc, args.strategy.upper(), model)}
-            log("cpu baseline (%d threads): %.0f reads/s (%d reads in %.1fs)" % (T, nt / ct, nt, ct))
+        cpu, cpu1 = cpu_baselines(oi, read_tuple, reads_per_step, gwa.STRATEGIES[args.strategy], args.k, args, O,
+                                  args.strategy.upper())
+    oi = None
 
     # Roofline of the dominant kernel.  `achieved` / `frac` follow SURVEY.md §8(d): 64 B per
     # reference FM step (one Occ block, the lower bound of §8d's 1-2 blocks), 4 B per SA gather, and
     # for each DP verification ceil(2n/8) + ceil(n/8) B of reference window + 32 B of Peq per 64-base
     # block.  `kernel_bytes` re-prices what the kernels actually read: 64 B per Occ block read, 8 B per
     # k-mer table lookup, 3/8 B per FM step answered from the 2-bit text (single-row interval).
-    steps = args.steps
-    q_ms, s_ms = qms / steps, sms / steps
+    q_ms, s_ms = kms["quickscan"], kms["search"]
     q_bytes = 64.0 * st.quick_blocks + 8.0 * st.kmer_lookups + 0.375 * st.quick_short_steps + 4.0 * st.quick_sa_reads
     q_ref = 64.0 * (st.quick_blocks + st.quick_short_steps) + 4.0 * st.quick_sa_reads
     s_bytes = (64.0 * (st.blocks - st.quick_blocks) + 0.375 * st.search_short_steps
@@ -389,13 +469,21 @@ def main():
                 % (gname, reads_per_step, m, "0-5 edits (subs/1-bp indels)" if c4 else "0-2 substitutions", args.k,
                    args.strategy))
     traffic, traffic_src = _pmc_traffic(dom, workload)
+    hg = None
+    if gen is not None and rank == 0:
+        batch.close()
+        gi.close()
+        del codes
+        hg = hg19r_leg(args, gen, gwa, synth, np, cfg, log)
     out = {
         "metric": METRIC if not c4 else "reads/sec, 150 bp k<=5 with indels vs hg19 (config C4)", "value": value,
-        "unit": "reads/s", "n_gpus": world, "steps": steps,
-        "warmup": args.warmup, "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
+        "unit": "reads/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-        "config": {"workload": workload,
-                   "genome_bp": int(len(codes)), "reads_per_gpu_per_step": reads_per_step,
+        "config": {"workload": workload, "timed_step": "encode the read text in HBM + fm_quickscan + %s_search tiers + "
+                                                      "SAM text written in HBM (gwa_batch_run + gwa_batch_format)"
+                                                      % args.strategy,
+                   "genome_bp": int(sum(lengths)), "reads_per_gpu_per_step": reads_per_step,
                    "parallelism": "reads sharded, index replicated (%d GPU)" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "definition": "SURVEY.md 8(d) algorithmic bytes",
                      "achieved": gbs(dom_ref, dom_ms), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -405,8 +493,10 @@ def main():
                      "kernel_bytes_frac": gbs(k_bytes, dom_ms) / HBM_PEAK_GBS},
         "cpu_baseline": cpu,
         "detail": {"rank_seconds": rank_times, "devices": "rank r on GPU r mod %d" % torch.cuda.device_count(),
-                   "timed_window_monotonic_ns": [win0, win1],
-                   "quickscan_ms": q_ms, "search_ms": s_ms, "kernel_ms": kms / steps,
+                   "timed_window_monotonic_ns": window,
+                   "encode_ms": kms["encode"], "quickscan_ms": q_ms, "search_ms": s_ms, "format_ms": kms["format"],
+                   "kernel_ms": kms["kernel"] + kms["format"], "sam_bytes_per_step": sam_bytes,
+                   "align_kernels_reads_per_s": reads_per_step / ((q_ms + s_ms) * 1e-3) if q_ms + s_ms > 0 else None,
                    "fm_searches_per_read": st.fm_searches / reads_per_step,
                    "quick_steps_per_read": st.quick_steps / reads_per_step,
                    "blocks_per_read": st.blocks / reads_per_step, "tier_reads": list(st.tier_reads),
@@ -422,11 +512,12 @@ def main():
                                    "traffic": _pmc_traffic("fm_quickscan", workload)[0],
                                    "gather_ceiling": gather_ceiling(st, q_ms)},
                    "mapped": st.n_mapped, "unmapped": st.n_unmapped, "index_build_s": t_index,
-                   "index_gb": gi.deviceBytes() / 1e9, "parity": parity},
+                   "index_gb": index_gb, "parity": parity, "hg19r": hg},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    batch.close()
+    if hg is None:
+        batch.close()
     if dist:
         tdist.destroy_process_group()
 
@@ -491,8 +582,8 @@ def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_i
         import oracle as O
         T, tdesc = host_cores()
         sa_f, sa_r = gi.suffixArray(0), gi.suffixArray(1)
-        O.check_cyclic_sa(codes, sa_f, samples=args.sa_check, seed=11, threads=T)
-        O.check_cyclic_sa(np.ascontiguousarray(codes[::-1]), sa_r, samples=args.sa_check, seed=12, threads=T)
+        O.check_cyclic_sa_full(codes, sa_f, threads=T)
+        O.check_cyclic_sa_full(np.ascontiguousarray(codes[::-1]), sa_r, threads=T)
         oi = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
         del sa_f, sa_r
         ocfg = O.OrcConfig.default(k=args.k)

@@ -108,6 +108,11 @@ struct gwa_batch {
   size_t fmtCap = 0, fmtTmpBytes = 0, fmtTextCap = 0;
   unsigned long long *d_stats = nullptr;
   bool statsDone = false;
+  // device encoding of the read text (gwa_batch_run re-encodes every run: the timed path starts
+  // from the text in HBM, as the reference's per-read call starts from the Read's String)
+  uint32_t *d_row = nullptr, *d_seen = nullptr;
+  void *d_encTmp = nullptr;
+  size_t encTmpBytes = 0;
   // device
   uint8_t *d_codes = nullptr;
   uint32_t *d_off = nullptr, *d_len = nullptr;
@@ -482,7 +487,8 @@ void gwa_free(void *p) { free(p); }
 static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
                 b->d_stair, b->d_stairBase, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
-                b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats};
+                b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
+                b->d_row, b->d_seen, b->d_encTmp};
   for (void *p : ps)
     if (p) (void)hipFree(p);
   // the text blobs (one allocation may back several of them)
@@ -538,26 +544,17 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   b->d_codes = devAlloc<uint8_t>(codeBound);
   b->d_off = devAlloc<uint32_t>((size_t)n + 1);
   b->d_len = devAlloc<uint32_t>((size_t)n + 1);
-  uint32_t *d_row = devAlloc<uint32_t>((size_t)n + 1);
-  uint32_t *d_seen = devAlloc<uint32_t>(kLenSeen);
-  const size_t tmpBytes = encodeScanTempBytes(n);
-  void *d_tmp = devAlloc<uint8_t>(tmpBytes);
+  b->d_row = devAlloc<uint32_t>((size_t)n + 1);
+  b->d_seen = devAlloc<uint32_t>(kLenSeen);
+  b->encTmpBytes = encodeScanTempBytes(n);
+  b->d_encTmp = devAlloc<uint8_t>(b->encTmpBytes);
+  // the length pass (read lengths, code offsets, the lengths present); gwa_batch_run encodes
   std::vector<uint32_t> seen(kLenSeen);
-  try {
-    HIPCHK(hipMemsetAsync(d_seen, 0, kLenSeen * sizeof(uint32_t), s));
-    launchEncode(b->d_seqText, b->d_seqB, b->d_seqE, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 0, s);
-    launchEncode(b->d_seqText, b->d_seqB, b->d_seqE, n, b->d_len, d_row, b->d_off, d_seen, b->d_codes, d_tmp, tmpBytes, 1, s);
-    HIPCHK(hipMemcpyAsync(seen.data(), d_seen, kLenSeen * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-  } catch (...) {
-    (void)hipFree(d_row);
-    (void)hipFree(d_seen);
-    (void)hipFree(d_tmp);
-    throw;
-  }
-  (void)hipFree(d_row);
-  (void)hipFree(d_seen);
-  (void)hipFree(d_tmp);
+  HIPCHK(hipMemsetAsync(b->d_seen, 0, kLenSeen * sizeof(uint32_t), s));
+  launchEncode(b->d_seqText, b->d_seqB, b->d_seqE, n, b->d_len, b->d_row, b->d_off, b->d_seen, b->d_codes, b->d_encTmp,
+               b->encTmpBytes, 0, s);
+  HIPCHK(hipMemcpyAsync(seen.data(), b->d_seen, kLenSeen * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   // the distinct read lengths: maximum length, k per length (AlignmentScoreConfig
   // .getMaximumEditDistance) and the staircase tables
   std::vector<int> lens;
@@ -836,6 +833,13 @@ int gwa_batch_run(gwa_batch_t *b) {
     ReadsView rv{b->d_codes, b->d_off, b->d_len, b->n};
     Events ev;
     hipEvent_t e0 = ev.e[0], e1 = ev.e[1], e2 = ev.e[2];
+    // encode the read text in HBM (ACGTSequence(String), A/ACGTSequence.java:86-97): lengths and
+    // code offsets, then the code rows
+    HIPCHK(hipEventRecord(e2, s));
+    launchEncode(b->d_seqText, b->d_seqB, b->d_seqE, b->n, b->d_len, b->d_row, b->d_off, b->d_seen, b->d_codes,
+                 b->d_encTmp, b->encTmpBytes, 0, s);
+    launchEncode(b->d_seqText, b->d_seqB, b->d_seqE, b->n, b->d_len, b->d_row, b->d_off, b->d_seen, b->d_codes,
+                 b->d_encTmp, b->encTmpBytes, 1, s);
     HIPCHK(hipMemsetAsync(b->d_count, 0, 16 * sizeof(uint32_t), s));
     HIPCHK(hipEventRecord(e0, s));
     const bool sf = b->cfg.strategy == 1;
@@ -847,9 +851,11 @@ int gwa_batch_run(gwa_batch_t *b) {
     uint32_t nSearch = b->n;
     if (!sf) HIPCHK(hipMemcpyAsync(&nSearch, b->d_count, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    float qms = 0;
+    float qms = 0, ems = 0;
     HIPCHK(hipEventElapsedTime(&qms, e0, e1));
+    HIPCHK(hipEventElapsedTime(&ems, e2, e0));
     b->stats.quickscan_ms = qms;
+    b->stats.encode_ms = ems;
     double searchMs = 0;
     int cur = 0;
     uint32_t n = nSearch;
@@ -971,7 +977,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       else if (!refused) break;
     }
     b->stats.search_ms = searchMs;
-    b->stats.kernel_ms = qms + searchMs;
+    b->stats.kernel_ms = ems + qms + searchMs;
     if (n > 0) throw std::runtime_error(std::to_string(n) + " reads exceeded the largest search tier");
     b->ran = true;
     return 0;
@@ -1067,6 +1073,8 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
     dIdx = b->d_fmtIdx;
   }
   HIPCHK(hipMemsetAsync(b->d_fmtErr, 0xFF, sizeof(uint32_t), s));
+  Events ev;
+  HIPCHK(hipEventRecord(ev.e[0], s));
   const SamText t = samText(b);
   const PairSpec ps{b->pairs, b->minIns, b->maxIns};
   size_t tmpBytes = b->fmtTmpBytes;
@@ -1102,6 +1110,11 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
   growDev(&b->d_fmtText, &b->fmtTextCap, (size_t)total + 1);
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
                   b->d_fmtErr, b->d_fmtText, 2, s, ps);
+  HIPCHK(hipEventRecord(ev.e[1], s));
+  HIPCHK(hipEventSynchronize(ev.e[1]));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]));
+  b->stats.format_ms = ms;
   return total;
 }
 

@@ -89,7 +89,7 @@ typedef struct {
 
 /* Per-batch counters (instrumentation for SURVEY.md §8d roofline accounting). */
 typedef struct {
-  double kernel_ms;        /* device time of all align kernels (HIP events) */
+  double kernel_ms;        /* device time of all kernels of gwa_batch_run: encode + align (HIP events) */
   double quickscan_ms;     /* fm_quickscan kernel */
   double search_ms;        /* bsf_search kernels (all tiers) */
   uint64_t fm_searches;    /* numFMIndexSearches summed over reads */
@@ -108,6 +108,8 @@ typedef struct {
   uint64_t num_sw;         /* DP verifications (alignBlockDetailed calls) */
   uint64_t verify_bytes;   /* SURVEY.md 8(d) bytes of those verifications (reference window + Peq) */
   uint64_t quick_text_runs; /* fm_quickscan text-mode runs (one 32-base 2-bit text window + N flags each) */
+  double encode_ms;        /* read encoding on the device at the start of gwa_batch_run (part of kernel_ms) */
+  double format_ms;        /* the last SAM formatting of the batch on the device (gwa_batch_format / results) */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);

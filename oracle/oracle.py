@@ -83,6 +83,7 @@ def lib():
             ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
         L.orc_check_cyclic_sa.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                           ctypes.c_uint64, ctypes.c_int]
+        L.orc_check_cyclic_sa_full.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -251,12 +252,25 @@ def revcomp(seq):
 
 
 def check_cyclic_sa(codes, sa, samples=1 << 20, seed=1, threads=16):
-    """Independent check of a cyclic suffix array of `codes` (permutation + sampled adjacent order);
-    raises AssertionError with the oracle's message on failure (orc_check_cyclic_sa)."""
+    """Independent check of a cyclic suffix array of `codes` (permutation + sampled adjacent order, by
+    direct rotation compares); raises AssertionError with the oracle's message on failure
+    (orc_check_cyclic_sa)."""
     import numpy as np
     codes = np.ascontiguousarray(codes, dtype=np.uint8)
     sa = np.ascontiguousarray(sa, dtype=np.uint32)
     assert len(sa) == len(codes)
     rc = lib().orc_check_cyclic_sa(codes.ctypes.data, len(codes), sa.ctypes.data, samples, seed, threads)
+    if rc != 0:
+        raise AssertionError("cyclic SA check failed: " + _err())
+
+
+def check_cyclic_sa_full(codes, sa, threads=16):
+    """Complete O(n) check of a cyclic suffix array (every adjacent pair, through the inverse
+    permutation: orc_check_cyclic_sa_full); raises AssertionError on failure."""
+    import numpy as np
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    sa = np.ascontiguousarray(sa, dtype=np.uint32)
+    assert len(sa) == len(codes)
+    rc = lib().orc_check_cyclic_sa_full(codes.ctypes.data, len(codes), sa.ctypes.data, threads)
     if rc != 0:
         raise AssertionError("cyclic SA check failed: " + _err())

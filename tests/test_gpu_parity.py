@@ -341,11 +341,11 @@ def hg19r_pair():
     import gwa
     codes, names, lengths = synth.genome_repeats(synth.HG19_CONTIGS, config_id=1, scale=0.005)
     gi = gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths)
-    # the oracle index takes the GPU suffix arrays after an independent check of them (permutation +
-    # 2^17 sampled adjacent pairs per strand; pairs inside segmental duplications compare ~100 kb)
+    # the oracle index takes the GPU suffix arrays after the complete independent check of them
+    # (permutation + every adjacent pair, orc_check_cyclic_sa_full)
     sa_f, sa_r = gi.suffixArray(0), gi.suffixArray(1)
-    O.check_cyclic_sa(codes, sa_f, samples=1 << 17)
-    O.check_cyclic_sa(np.ascontiguousarray(codes[::-1]), sa_r, samples=1 << 17)
+    O.check_cyclic_sa_full(codes, sa_f)
+    O.check_cyclic_sa_full(np.ascontiguousarray(codes[::-1]), sa_r)
     oi = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
     return codes, lengths, gi, oi
 

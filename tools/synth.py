@@ -161,6 +161,35 @@ def genome_repeats(contigs, config_id=1, scale=1.0, log=None):
     return codes, names, lengths
 
 
+def genome_ngaps(contigs, config_id=1, scale=1.0):
+    """The BASELINE stand-in: i.i.d. uniform ACGT at the given contig lengths with
+    hg19-like N-gap runs and no repeats -> (codes, names, lengths).  Gaps per chromosome as in
+    genome_repeats: 10 kb telomeres, a 3 Mb centromere (chromosomes >= 20 Mb), the acrocentric short
+    arms, chrY heterochromatin, ~8 scattered 50-100 kb gaps (about 6 % N at hg19 size).
+    Deterministic for (contigs, config_id, scale)."""
+    codes, names, lengths = genome(contigs, config_id, scale)
+    rng = np.random.Generator(np.random.PCG64(SEED0 ^ (config_id + 0x6A95)))
+    o = 0
+    for nm, L in zip(names, lengths):
+        tel = min(10000, L // 20)
+        codes[o:o + tel] = 4
+        codes[o + L - tel:o + L] = 4
+        if L >= 5e6 * scale or L >= 2e7:
+            if nm in _ACRO:
+                codes[o:o + int(_ACRO[nm] * scale)] = 4
+            if nm == "chrY":
+                a = o + int(0.45 * L)
+                codes[a:a + int(0.5 * L)] = 4
+            cen = o + int(L * rng.uniform(0.3, 0.55))
+            codes[cen:cen + int(3.0e6 * scale)] = 4
+            for _ in range(int(rng.poisson(8))):
+                gl = int(rng.integers(50000, 100000) * scale)
+                a = o + int(rng.random() * max(1, L - gl))
+                codes[a:a + gl] = 4
+        o += L
+    return codes, names, lengths
+
+
 def reads(codes, lengths, n, m=100, max_subs=2, config_id=2, shard=0, indels=False, max_edits=5):
     """-> (seqs uint8 [n, m] codes, names list) ; substitutions: #subs uniform {0..max_subs},
     distinct positions, base uniform over the other 3."""
@@ -289,3 +318,12 @@ def fasta_text(codes, names, lengths, width=60):
         parts.extend(s[i:i + width] + "\n" for i in range(0, L, width))
         off += L
     return "".join(parts)
+
+
+if __name__ == "__main__":
+    # python tools/synth.py hg19r|hg19 OUT.npy : write a genome's codes (bench.py generates the hg19r
+    # leg's genome in a child process while its main leg runs)
+    import sys
+    kind, out = sys.argv[1], sys.argv[2]
+    c, _, _ = (genome_repeats if kind == "hg19r" else genome_ngaps)(HG19_CONTIGS, config_id=1)
+    np.save(out, c)
