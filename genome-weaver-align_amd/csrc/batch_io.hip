@@ -24,6 +24,7 @@
 
 #include "kernels.h"
 #include "sam_core.h"
+#include "text_core.h"
 
 namespace gwa {
 
@@ -45,6 +46,34 @@ __device__ __forceinline__ uint8_t to3bitDev(unsigned char c) {
   }
 }
 
+// Read text loads: 16-B aligned chunks (the text allocations are padded by 32 bytes, so the chunk
+// holding a field's last byte is always inside the allocation) funnel-shifted to the field start.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 loadChunk(const char *__restrict__ base, uint64_t a16) {
+  return *reinterpret_cast<const u32x4 *>(base + a16);
+}
+// bytes [p, p + 16) of the text as 4 dwords (p any alignment)
+__device__ __forceinline__ void load16(const char *__restrict__ t, uint64_t p, uint32_t (&w)[4]) {
+  const uint64_t a = p & ~(uint64_t)15;
+  const int sh = (int)(p & 15);
+  const u32x4 c0 = loadChunk(t, a);
+  uint32_t x[8] = {c0.x, c0.y, c0.z, c0.w, 0, 0, 0, 0};
+  if (sh) {
+    const u32x4 c1 = loadChunk(t, a + 16);
+    x[4] = c1.x; x[5] = c1.y; x[6] = c1.z; x[7] = c1.w;
+  }
+  const int q = sh >> 2, r = (sh & 3) * 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // dwords q + i and q + i + 1 (q = 0..3) through selects
+    uint32_t lo = x[i], hi = x[i + 1];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      lo = q == k ? x[k + i] : lo;
+      hi = q == k ? x[k + i + 1] : hi;
+    }
+    w[i] = r ? (lo >> r) | (hi << (32 - r)) : lo;
+  }
+}
 // per read: bases after skipping spaces, its padded row size, and a mark in the length table
 __global__ void __launch_bounds__(256) encodeLenKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqB,
                                                        const uint64_t *__restrict__ seqE, uint32_t n, uint32_t *__restrict__ codeLen,
@@ -55,24 +84,62 @@ __global__ void __launch_bounds__(256) encodeLenKernel(const char *__restrict__ 
     rowLen[n] = 16;
     return;
   }
-  uint32_t m = 0;
-  for (uint64_t i = seqB[r]; i < seqE[r]; ++i) m += seq[i] != ' ';
+  const uint64_t b = seqB[r], e = seqE[r];
+  uint32_t spaces = 0;
+  // aligned 16-B chunks over [b, e); bytes outside the field are masked off
+  for (uint64_t a = b & ~(uint64_t)15; a < e; a += 16) {
+    const u32x4 c = loadChunk(seq, a);
+    const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t p = a + 4 * i;
+      uint32_t m = bytesEq(w[i], ' ');
+      // keep bytes p + j with b <= p + j < e
+      const int64_t lo = (int64_t)b - (int64_t)p, hi = (int64_t)e - (int64_t)p;
+      const uint32_t keepLo = lo <= 0 ? 0xFFFFFFFFu : lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo));
+      const uint32_t keepHi = hi >= 4 ? 0xFFFFFFFFu : hi <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - hi)));
+      spaces += __builtin_popcount(m & keepLo & keepHi);
+    }
+  }
+  const uint32_t m = (uint32_t)(e - b) - spaces;
   codeLen[r] = m;
   rowLen[r] = (m + 15) & ~15u;
   lenSeen[m < kLenSeen - 1 ? m : kLenSeen - 1] = 1;
 }
 
+// one read's code row: 16 codes per store (rows are 16-B aligned and zero-padded); a read with
+// spaces in its text (skipped, A/ACGTSequence.java:86-97) takes the byte loop
 __global__ void __launch_bounds__(256) encodeWriteKernel(const char *__restrict__ seq, const uint64_t *__restrict__ seqB,
                                                          const uint64_t *__restrict__ seqE, uint32_t n,
                                                          const uint32_t *__restrict__ codeOff,
+                                                         const uint32_t *__restrict__ codeLen,
                                                          uint8_t *__restrict__ codes) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   uint8_t *o = codes + codeOff[r];
+  const uint64_t b = seqB[r], e = seqE[r];
+  const uint32_t m = codeLen[r], row = codeOff[r + 1] - codeOff[r];
+  if (m == e - b) {
+    for (uint32_t k = 0; k < row; k += 16) {
+      uint32_t w[4];
+      load16(seq, b + k, w);
+      u32x4 v;
+      uint32_t c[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int valid = (int)m - (int)(k + 4 * i);  // bytes of this dword inside the read
+        const uint32_t keep = valid >= 4 ? 0xFFFFFFFFu : valid <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - valid)));
+        c[i] = to3bit4(w[i]) & keep;
+      }
+      v.x = c[0]; v.y = c[1]; v.z = c[2]; v.w = c[3];
+      *reinterpret_cast<u32x4 *>(o + k) = v;
+    }
+    return;
+  }
   uint32_t k = 0;
-  for (uint64_t i = seqB[r]; i < seqE[r]; ++i)
+  for (uint64_t i = b; i < e; ++i)
     if (seq[i] != ' ') o[k++] = to3bitDev((unsigned char)seq[i]);
-  for (const uint32_t e = codeOff[r + 1] - codeOff[r]; k < e; ++k) o[k] = 0;
+  for (; k < row; ++k) o[k] = 0;
 }
 
 void launchEncode(const char *seq, const uint64_t *seqB, const uint64_t *seqE, uint32_t n, uint32_t *codeLen, uint32_t *rowLen,
@@ -85,7 +152,7 @@ void launchEncode(const char *seq, const uint64_t *seqB, const uint64_t *seqE, u
     size_t b = scanTmpBytes;
     FCHK(rocprim::exclusive_scan(scanTmp, b, rowLen, codeOff, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), s));
   } else {
-    hipLaunchKernelGGL(encodeWriteKernel, grid, dim3(256), 0, s, seq, seqB, seqE, n, codeOff, codes);
+    hipLaunchKernelGGL(encodeWriteKernel, grid, dim3(256), 0, s, seq, seqB, seqE, n, codeOff, codeLen, codes);
     FCHK(hipGetLastError());
   }
 }
@@ -178,15 +245,45 @@ __global__ void __launch_bounds__(256) samLenKernel(SamText t, const OutHeader *
   len[j] = o.n;
 }
 
-__global__ void __launch_bounds__(256) samWriteKernel(SamText t, const OutHeader *__restrict__ oh, const OutHit *__restrict__ hits,
-                                                      const uint16_t *__restrict__ cig, const uint32_t *__restrict__ idx,
-                                                      uint32_t first, uint32_t n, const uint64_t *__restrict__ off,
-                                                      char *__restrict__ out, PairSpec ps) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t r = idx ? idx[j] : first + j;
-  SamOut o{out + off[j], 0};
-  (void)samUnit(o, t, r, oh, hits, cig, ps);
+// Write pass.  The text of a workgroup's 64 units is one contiguous range of the output
+// [off[j0], off[j0 + 64]); it is formatted into LDS (byte stores that stay on the CU) at the
+// position it has relative to the 16-B aligned start of that range, then copied out with coalesced
+// 16-B stores (the two partial chunks at the range's ends are written bytewise, the neighbouring
+// workgroups own their other bytes).  A range larger than the staging buffer (many reported lines)
+// is written directly to HBM.
+template <int STAGE>
+__global__ void __launch_bounds__(64) samWriteKernel(SamText t, const OutHeader *__restrict__ oh, const OutHit *__restrict__ hits,
+                                                     const uint16_t *__restrict__ cig, const uint32_t *__restrict__ idx,
+                                                     uint32_t first, uint32_t n, const uint64_t *__restrict__ off,
+                                                     char *__restrict__ out, PairSpec ps) {
+  __shared__ u32x4 stage[STAGE / 16];
+  const uint32_t j0 = blockIdx.x * 64, j = j0 + threadIdx.x;
+  const uint32_t jEnd = j0 + 64 < n ? j0 + 64 : n;
+  const uint64_t gBeg = off[j0], gEnd = off[jEnd];
+  const uint64_t base = gBeg & ~(uint64_t)15;
+  if (gEnd - base > (uint64_t)STAGE) {
+    if (j < n) {
+      SamOut o{out + off[j], 0};
+      (void)samUnit(o, t, idx ? idx[j] : first + j, oh, hits, cig, ps);
+    }
+    return;
+  }
+  if (j < n) {
+    SamOut o{reinterpret_cast<char *>(stage) + (off[j] - base), 0};
+    (void)samUnit(o, t, idx ? idx[j] : first + j, oh, hits, cig, ps);
+  }
+  __syncthreads();
+  const uint32_t chunks = (uint32_t)((gEnd - base + 15) >> 4);
+  for (uint32_t c = threadIdx.x; c < chunks; c += 64) {
+    const uint64_t a = base + 16ull * c;
+    if (a >= gBeg && a + 16 <= gEnd) {
+      *reinterpret_cast<u32x4 *>(out + a) = stage[c];
+    } else {
+      const char *sb = reinterpret_cast<const char *>(stage) + 16ull * c;
+      for (int i = 0; i < 16; ++i)
+        if (a + i >= gBeg && a + i < gEnd) out[a + i] = sb[i];
+    }
+  }
 }
 
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
@@ -199,7 +296,13 @@ void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, 
   } else if (pass == 1) {  // exclusive scan of n + 1 lengths: off[n] = total bytes
     FCHK(rocprim::exclusive_scan(scanTmp, *scanTmpBytes, len, off, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), s));
   } else {
-    hipLaunchKernelGGL(samWriteKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
+    if (n == 0) return;
+    const dim3 g64((n + 63) / 64);
+    // 24 KiB of staging (6 workgroups per CU) holds 64 single-end 100-150 bp records; pairs get 48 KiB
+    if (ps.np)
+      hipLaunchKernelGGL(samWriteKernel<49152>, g64, dim3(64), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
+    else
+      hipLaunchKernelGGL(samWriteKernel<24576>, g64, dim3(64), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
     FCHK(hipGetLastError());
   }
 }

@@ -99,6 +99,7 @@ struct gwa_batch {
   char *d_seqText = nullptr, *d_nameText = nullptr, *d_qualText = nullptr;
   const uint64_t *d_seqB = nullptr, *d_seqE = nullptr, *d_nameB = nullptr, *d_nameE = nullptr;
   const uint64_t *d_qualB = nullptr, *d_qualE = nullptr;
+  uint8_t *d_qualNull = nullptr;  // per read: nonzero = no quality (gwa_reads_t.qual_null), or nullptr
   uint64_t *d_fieldOwn[3] = {nullptr, nullptr, nullptr};  // the allocations behind the field arrays
   // SAM formatting buffers (grown on demand) and the statistics accumulator
   uint64_t *d_fmtLen = nullptr, *d_fmtOff = nullptr;
@@ -488,7 +489,7 @@ static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
                 b->d_stair, b->d_stairBase, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
-                b->d_row, b->d_seen, b->d_encTmp};
+                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull};
   for (void *p : ps)
     if (p) (void)hipFree(p);
   // the text blobs (one allocation may back several of them)
@@ -634,7 +635,7 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
       std::vector<uint64_t> o(off, off + n + 1);
       const uint64_t o0 = o[0];
       for (auto &x : o) x -= o0;
-      *dText = devAlloc<char>(o[n] + 1);
+      *dText = devAlloc<char>(o[n] + 32);  // (+32: the device reads the text in aligned 16-B chunks)
       if (o[n]) HIPCHK(hipMemcpyAsync(*dText, base + o0, o[n], hipMemcpyHostToDevice, s));
       *dOff = devUpload(o, s, nullptr);
       HIPCHK(hipStreamSynchronize(s));  // (o is a local vector)
@@ -654,6 +655,11 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
       b->d_fieldOwn[2] = off;
       b->d_qualB = off;
       b->d_qualE = off + 1;
+      if (reads->qual_null) {  // reads without a quality among reads with one
+        b->d_qualNull = devAlloc<uint8_t>(n);
+        if (n) HIPCHK(hipMemcpyAsync(b->d_qualNull, reads->qual_null, n, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+      }
     }
     batchTail(b, seqBytes);
     *out = b;
@@ -682,7 +688,7 @@ int batchCreateFastq(gwa_index_t *ix, const gwa_config_t *cfg, const char *text,
     }
     b->hasQual = true;
     hipStream_t s = b->stream;
-    char *dText = devAlloc<char>(len + 1);
+    char *dText = devAlloc<char>(len + 32);  // (+32: the device reads the text in aligned 16-B chunks)
     b->d_seqText = dText;
     HIPCHK(hipMemcpyAsync(dText, text, len, hipMemcpyHostToDevice, s));
     uint64_t *dStart = devAlloc<uint64_t>(n);
@@ -1025,6 +1031,7 @@ static SamText samText(const gwa_batch *b) {
   t.qual = b->hasQual ? b->d_qualText : nullptr;
   t.qualB = b->d_qualB;
   t.qualE = b->d_qualE;
+  t.qualNull = b->d_qualNull;
   t.codes = b->d_codes;
   t.codeOff = b->d_off;
   t.codeLen = b->d_len;
@@ -1126,6 +1133,7 @@ static void formatResults(gwa_batch *b, const uint32_t *hostIdx, uint32_t first,
   out->line_off = nullptr;
   out->records = nullptr;
   out->n_records = 0;
+  out->paired = b->pairs ? 1 : 0;
   if (b->headerOnly) {
     if (!b->ran) throw std::runtime_error("gwa_batch_run has not completed");
     out->sam = (char *)calloc(1, 1);
@@ -1211,7 +1219,6 @@ int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_r
                            int32_t min_insert, int32_t max_insert, gwa_batch_t **out) {
   try {
     if (mate1->n != mate2->n) throw std::runtime_error("paired-end: the mate files hold different numbers of reads");
-    if ((mate1->qual == nullptr) != (mate2->qual == nullptr)) throw std::runtime_error("paired-end: qualities for one mate only");
     if (cfg->strategy != 0) throw std::runtime_error("paired-end alignment runs the -m bsf search");
     if (min_insert < 0 || max_insert < min_insert) throw std::runtime_error("bad insert-size range");
     // one batch of 2n single-end reads: mate 1 of every pair, then mate 2
@@ -1219,12 +1226,18 @@ int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_r
     std::string blob[3];
     std::vector<uint64_t> off[3];
     const gwa_reads_t *ms[2] = {mate1, mate2};
+    const bool anyQual = mate1->qual || mate2->qual;
+    std::vector<uint8_t> qnull;  // per read of the combined batch: no quality
     for (int f = 0; f < 3; ++f) {
-      if (f == 2 && !mate1->qual) break;
+      if (f == 2 && !anyQual) break;
       off[f].reserve(2 * (size_t)n + 1);
       off[f].push_back(0);
       for (int k = 0; k < 2; ++k) {
         const gwa_reads_t *r = ms[k];
+        if (f == 2 && !r->qual) {  // this mate set has no qualities: empty ranges, marked null
+          for (uint32_t i = 1; i <= n; ++i) off[f].push_back(off[f].back());
+          continue;
+        }
         const char *base = f == 0 ? r->name : f == 1 ? r->seq : r->qual;
         const uint64_t *o = f == 0 ? r->name_off : f == 1 ? r->seq_off : r->qual_off;
         blob[f].append(base + o[0], o[n] - o[0]);
@@ -1232,8 +1245,14 @@ int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_r
         for (uint32_t i = 1; i <= n; ++i) off[f].push_back(at + (o[i] - o[0]));
       }
     }
-    gwa_reads_t both{2 * n, blob[0].data(), blob[1].data(), mate1->qual ? blob[2].data() : nullptr, off[0].data(),
-                     off[1].data(), mate1->qual ? off[2].data() : nullptr};
+    if (anyQual && (!mate1->qual || !mate2->qual || mate1->qual_null || mate2->qual_null)) {
+      qnull.assign(2 * (size_t)n, 0);
+      for (int k = 0; k < 2; ++k)
+        for (uint32_t i = 0; i < n; ++i)
+          qnull[(size_t)k * n + i] = !ms[k]->qual ? 1 : (ms[k]->qual_null && ms[k]->qual_null[i]) ? 1 : 0;
+    }
+    gwa_reads_t both{2 * n, blob[0].data(), blob[1].data(), anyQual ? blob[2].data() : nullptr, off[0].data(),
+                     off[1].data(), anyQual ? off[2].data() : nullptr, qnull.empty() ? nullptr : qnull.data()};
     gwa_config_t c = *cfg;
     c.report_type = 1;  // every best hit of a mate is a pairing candidate
     if (gwa_batch_create(ix, &c, &both, out) != 0) return -1;
@@ -1370,13 +1389,15 @@ int gwa_results_records(const gwa_index_t *ix, gwa_results_t *r) {
           else if (f[k].second >= 5 && !memcmp(p, "X0:i:", 5)) g.x0 = (int32_t)strtol(std::string(p + 5, f[k].second - 5).c_str(), nullptr, 10);
           else if (f[k].second >= 5 && !memcmp(p, "XP:Z:", 5)) { g.state_off = f[k].first + 5; g.state_len = (uint32_t)(f[k].second - 5); }
         }
-        // a first line with FLAG 0x1 and without 0x80 is followed by its split record
-        if (!recs.empty() && recs.back().split == -2) {
+        // single-end results: a first line with FLAG 0x1 and without 0x80 is followed by its split
+        // record (AlignmentRecord.toSAMLine, R/AlignmentRecord.java:109-170); paired-end results have
+        // two mate lines per unit and no split records
+        if (!r->paired && !recs.empty() && recs.back().split == -2) {
           gwa_record_t &first = recs.back();
           first.split = (int32_t)recs.size();
           g.is_split = 1;
         }
-        if ((g.flag & 0x1) && !(g.flag & 0x80) && !g.is_split) {
+        if (!r->paired && (g.flag & 0x1) && !(g.flag & 0x80) && !g.is_split) {
           g.split = -2;  // (resolved by the next line)
           g.end = g.pos;
         }

@@ -165,8 +165,23 @@ struct Result {
 
 }  // namespace
 
-// read-file chunks (and the room before each for the records carried over from the previous one)
+// read-file chunks (and the room before each for the records carried over from the previous one);
+// a smaller file reads in one chunk of its own size
 constexpr uint64_t kChunk = 256ull << 20, kReserve = 512ull << 20;
+
+namespace {
+// MemAvailable of /proc/meminfo in bytes (0 = unknown)
+uint64_t memAvailable() {
+  FILE *f = fopen("/proc/meminfo", "r");
+  if (!f) return 0;
+  char line[256];
+  uint64_t kb = 0;
+  while (fgets(line, sizeof line, f))
+    if (sscanf(line, "MemAvailable: %lu kB", (unsigned long *)&kb) == 1) break;
+  fclose(f);
+  return kb * 1024;
+}
+}  // namespace
 
 struct gwa_pipeline {
   std::vector<gwa_index_t *> ix;
@@ -175,6 +190,7 @@ struct gwa_pipeline {
   int workersPerDevice = 2;
   gwa_pipeline_stats_t stats{};
   BufPool pool;  // pinned read-text buffers, kept across align_file calls
+  uint64_t pinnedBufs = 0, pinnedBytes = 0;  // pinned so far (lazily, by align_file)
   std::mutex samMu;
   std::vector<std::pair<char *, uint64_t>> samBufs;  // pinned SAM buffers, one per file worker, kept too
   ~gwa_pipeline() {
@@ -462,15 +478,6 @@ int gwa_pipeline_open(gwa_index_t *const *ix, int n_ix, const gwa_config_t *cfg,
     p->cfg = *cfg;
     p->batchReads = batch_reads ? batch_reads : (1u << 20);
     p->workersPerDevice = workers_per_device > 0 ? workers_per_device : 3;
-    // Pin the read-text buffers a file run keeps in flight (read-ahead, the chunk being framed, the
-    // batches in the workers) now: pinning while batches run stalls their copies in the runtime
-    // (measured: FASTQ -> SAM 8 M reads/s with background pinning, 20-25 M with the buffers pinned
-    // first).  Without pinned memory, runs use pageable buffers.
-    const size_t nbuf = 4 + (size_t)n_ix * (size_t)p->workersPerDevice;
-    try {
-      for (size_t i = 0; i < nbuf; ++i) p->pool.addPinned(kReserve + kChunk);
-    } catch (std::exception &) {
-    }
     *out = p;
     return 0;
   } catch (std::exception &e) {
@@ -487,12 +494,13 @@ int gwa_pipeline_stats(const gwa_pipeline_t *p, gwa_pipeline_stats_t *st) {
 
 int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_t *out) {
   Run run(p);
+  std::thread feeder;
   try {
     const auto t0 = Clock::now();
     const uint32_t n = reads->n;
     const uint64_t nb = ((uint64_t)n + p->batchReads - 1) / p->batchReads;
     run.start();
-    std::thread feeder([&] {
+    feeder = std::thread([&] {
       for (uint64_t i = 0; i < nb; ++i) {
         Job j;
         j.id = i;
@@ -502,6 +510,7 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
         j.reads.name_off = reads->name_off + a;
         j.reads.seq_off = reads->seq_off + a;
         j.reads.qual_off = reads->qual ? reads->qual_off + a : nullptr;
+        j.reads.qual_null = reads->qual && reads->qual_null ? reads->qual_null + a : nullptr;
         if (!run.push(std::move(j))) break;
       }
       run.finishJobs();
@@ -524,6 +533,7 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
     out->n_reads = n;
     out->records = nullptr;
     out->n_records = 0;
+    out->paired = 0;
     out->sam = (char *)malloc(total + 1);
     out->sam_len = total;
     out->line_off = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n + 1));
@@ -544,7 +554,8 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
     for (size_t d = 0; d < p->ix.size() && d < 16; ++d) p->stats.device_kernel_s[d] = run.devBusy[d];
     return 0;
   } catch (std::exception &e) {
-    run.fail(e.what());
+    run.fail(e.what());  // (wakes a feeder blocked in push)
+    if (feeder.joinable()) feeder.join();
     run.join();
     return gwa_fail_message(e.what());
   }
@@ -569,8 +580,37 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
     struct stat sb;
     const off_t pos0 = ::lseek(fd, 0, SEEK_CUR);
     run.fd = fd;
-    run.seekable = pos0 >= 0 && ::fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+    // batches are written at their offsets (pwrite) only to a regular file opened without O_APPEND:
+    // pwrite ignores the offset under O_APPEND (Linux) and would append in completion order
+    const int fl = ::fcntl(fd, F_GETFL);
+    run.seekable = pos0 >= 0 && fl >= 0 && !(fl & O_APPEND) && ::fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
     run.base = run.seekable ? (uint64_t)pos0 : 0;
+    // chunk size: the whole file when it is smaller than kChunk (plain files; .gz sizes are unknown)
+    uint64_t fileBytes = 0;
+    {
+      struct stat st;
+      if (!gz && ::fstat(in, &st) == 0 && S_ISREG(st.st_mode)) fileBytes = (uint64_t)st.st_size;
+    }
+    const uint64_t chunk = fileBytes ? std::min<uint64_t>(kChunk, ((fileBytes >> 20) + 1) << 20) : kChunk;
+    const uint64_t reserve = std::min<uint64_t>(kReserve, 2 * chunk);
+    // Pin the read-text buffers this run keeps in flight (read-ahead, the chunk being framed, the
+    // batches in the workers) before it starts -- pinning while batches run stalls their copies in
+    // the runtime (measured: FASTQ -> SAM 8 M reads/s with background pinning, 20-25 M with the
+    // buffers pinned first) -- as many as the file needs, at most a quarter of the available host
+    // memory, kept for later calls.  Beyond them runs use pageable buffers.
+    {
+      const uint64_t nbuf = 4 + (uint64_t)p->ix.size() * (uint64_t)p->workersPerDevice;
+      const uint64_t need = fileBytes ? std::min<uint64_t>(nbuf, fileBytes / chunk + 3) : nbuf;
+      const uint64_t avail = memAvailable(), capB = avail ? avail / 4 : (8ull << 30);
+      try {
+        while (p->pinnedBufs < need && p->pinnedBytes + reserve + chunk <= capB) {
+          p->pool.addPinned(reserve + chunk);
+          ++p->pinnedBufs;
+          p->pinnedBytes += reserve + chunk;
+        }
+      } catch (std::exception &) {  // (pinning failed: pageable buffers)
+      }
+    }
     const auto t0 = Clock::now();
     double readS = 0, frameS = 0;
     run.startFile();
@@ -581,8 +621,6 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
     // room where this thread puts the records carried over from the previous chunk; this thread frames
     // each chunk into batches of complete records (FASTQ: every record's header offset) while the IO
     // thread reads the next.  Only full batches leave a chunk unless the file has ended.
-    const uint64_t chunk = kChunk;
-    const uint64_t reserve = kReserve;
     const unsigned nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     struct Chunk {
       std::shared_ptr<TextBuf> buf;

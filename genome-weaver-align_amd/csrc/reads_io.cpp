@@ -42,10 +42,17 @@ struct Lines {
   bool final;
   bool next(uint64_t *b, uint64_t *e) {
     if (pos >= len) return false;
-    // the next "\n" (memchr), unless a "\r" comes first
-    const char *nl = (const char *)memchr(t + pos, '\n', len - pos);
-    uint64_t i = nl ? (uint64_t)(nl - t) : len;
-    if (const char *cr = (const char *)memchr(t + pos, '\r', i - pos)) i = (uint64_t)(cr - t);
+    // the first "\n" or "\r" from pos: memchr over growing windows, so a text with "\r" line ends
+    // only is scanned once (a "\n" search to the end of the text per line would be quadratic)
+    uint64_t i = pos;
+    for (uint64_t w = 256;; w *= 2) {
+      const uint64_t end = std::min<uint64_t>(len, i + w);
+      const char *nl = (const char *)memchr(t + i, '\n', end - i);
+      const uint64_t lim = nl ? (uint64_t)(nl - t) : end;
+      if (const char *cr = (const char *)memchr(t + i, '\r', lim - i)) { i = (uint64_t)(cr - t); break; }
+      if (nl || end == len) { i = lim; break; }
+      i = end;
+    }
     if (i == len) {
       if (!final) return false;
       *b = pos; *e = len; pos = len;
@@ -363,6 +370,7 @@ extern "C" int gwa_reads_parse(const char *text, uint64_t len, int format, int f
     out->reads.seq_off = b->seqOff.data();
     out->reads.qual = format == 1 ? b->qual.data() : nullptr;
     out->reads.qual_off = format == 1 ? b->qualOff.data() : nullptr;
+    out->reads.qual_null = nullptr;
     *consumed = done;
     return 0;
   } catch (std::exception &e) {

@@ -19,6 +19,7 @@ struct SamText {
   const uint64_t *nameB, *nameE;
   const char *qual;          // nullptr: no qualities (SAM "*", as for FASTA input)
   const uint64_t *qualB, *qualE;
+  const uint8_t *qualNull;   // nullptr, or per read: nonzero = this read's quality is null ("*")
   const uint8_t *codes;      // ReadsView: the read as codes 0..4 (spaces skipped)
   const uint32_t *codeOff, *codeLen;
   const char *ctg;           // contig names
@@ -57,6 +58,9 @@ struct SamOut {
     while (k) ch(b[--k]);
   }
 };
+
+// Read.getQual(0) == null for read r: the batch has no qualities or this read has none
+GWA_HD bool qualAbsent(const SamText &t, uint32_t r) { return t.qual == nullptr || (t.qualNull && t.qualNull[r]); }
 
 namespace samfmt {
 
@@ -239,7 +243,7 @@ GWA_HD void emitRec(SamOut &o, Ctx &cx, const Rec &r, const Rec *split, bool has
 GWA_HD int samChain(SamOut &o, const SamText &t, uint32_t r, const OutHit *hits, const uint16_t *cig, int head) {
   using namespace samfmt;
   const OutHit &h = hits[head];
-  Ctx cx{t, r, hits, (int)t.codeLen[r], h.strand != 0 ? 1 : 0, t.qual == nullptr, 0, 0};
+  Ctx cx{t, r, hits, (int)t.codeLen[r], h.strand != 0 ? 1 : 0, qualAbsent(t, r), 0, 0};
   if (!cx.qualNull) {
     cx.q0 = t.qualB[r];
     cx.qn = t.qualE[r] - t.qualB[r];
@@ -326,7 +330,7 @@ GWA_HD void samUnmapped(SamOut &o, const SamText &t, uint32_t r) {
   const uint8_t *c = t.codes + t.codeOff[r];
   for (uint32_t j = 0; j < t.codeLen[r]; ++j) o.ch(samfmt::kSym[c[j] > 4 ? 4 : c[j]]);
   o.ch('\t');
-  if (t.qual) o.bytes(t.qual + t.qualB[r], t.qualE[r] - t.qualB[r]);
+  if (!qualAbsent(t, r)) o.bytes(t.qual + t.qualB[r], t.qualE[r] - t.qualB[r]);
   else o.ch('*');
   o.ch('\n');
 }
@@ -411,7 +415,7 @@ GWA_HD void samMateLine(SamOut &o, const SamText &t, uint32_t r, const OutHit *h
     o.ch(samfmt::kSym[!rev ? (x > 4 ? 4 : x) : (x < 4 ? 3 - x : 4)]);
   }
   o.ch('\t');
-  if (!t.qual) {
+  if (qualAbsent(t, r)) {
     o.ch('*');
   } else {
     const uint64_t q0 = t.qualB[r], qn = t.qualE[r] - t.qualB[r];

@@ -28,7 +28,8 @@ class _Config(ctypes.Structure):
 
 class _Reads(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32), ("name", ctypes.c_void_p), ("seq", ctypes.c_void_p), ("qual", ctypes.c_void_p),
-                ("name_off", ctypes.c_void_p), ("seq_off", ctypes.c_void_p), ("qual_off", ctypes.c_void_p)]
+                ("name_off", ctypes.c_void_p), ("seq_off", ctypes.c_void_p), ("qual_off", ctypes.c_void_p),
+                ("qual_null", ctypes.c_void_p)]
 
 
 class _ReadBuf(ctypes.Structure):
@@ -45,7 +46,8 @@ class Record(ctypes.Structure):
 
 class _Results(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_uint32), ("sam", ctypes.c_void_p), ("sam_len", ctypes.c_uint64),
-                ("line_off", ctypes.c_void_p), ("records", ctypes.c_void_p), ("n_records", ctypes.c_uint64)]
+                ("line_off", ctypes.c_void_p), ("records", ctypes.c_void_p), ("n_records", ctypes.c_uint64),
+                ("paired", ctypes.c_uint32)]
 
 
 class BatchStats(ctypes.Structure):
@@ -254,23 +256,27 @@ class FMIndexOnGenome:
 
 
 def _reads_struct(reads, keep):
+    """gwa_reads_t of [(name, seq, qual-or-None)]: a read whose qual is None prints QUAL "*" (the
+    reference's Read.getQual(0) == null, R/AlignmentRecord.java:157), per read (qual_null)."""
+    import numpy as np
     names, seqs, quals = zip(*reads) if reads else ((), (), ())
     nb, no = _pack(names)
     sb, so = _pack(seqs)
-    has_q = len(reads) > 0 and all(q is not None for q in quals)
-    if any(q is not None for q in quals) and not has_q:
-        raise GwaError("a batch must have qualities for every read or for none")
+    any_q = any(q is not None for q in quals)
     r = _Reads()
     r.n = len(reads)
     keep.extend([nb, no, sb, so])
     r.name, r.seq = ctypes.cast(ctypes.c_char_p(nb), ctypes.c_void_p), ctypes.cast(ctypes.c_char_p(sb), ctypes.c_void_p)
     r.name_off, r.seq_off = no.ctypes.data, so.ctypes.data
-    if has_q:
-        qb, qo = _pack(quals)
+    r.qual, r.qual_off, r.qual_null = None, None, None
+    if any_q:
+        qb, qo = _pack([q if q is not None else "" for q in quals])
         keep.extend([qb, qo])
         r.qual, r.qual_off = ctypes.cast(ctypes.c_char_p(qb), ctypes.c_void_p), qo.ctypes.data
-    else:
-        r.qual, r.qual_off = None, None
+        if any(q is None for q in quals):
+            qn = np.array([q is None for q in quals], dtype=np.uint8)
+            keep.append(qn)
+            r.qual_null = qn.ctypes.data
     return r
 
 
@@ -329,6 +335,7 @@ class ParsedReads:
         r.name_off = r0.name_off + 8 * first
         r.seq_off = r0.seq_off + 8 * first
         r.qual_off = (r0.qual_off + 8 * first) if r0.qual_off else None
+        r.qual_null = (r0.qual_null + first) if r0.qual_null else None
         return r
 
     def records(self):

@@ -39,11 +39,15 @@ typedef struct {
 } gwa_config_t;
 
 /* A batch of reads, SoA, caller-owned.  Read i = name[name_off[i], name_off[i+1]), etc.
- * qual may be NULL (SAM QUAL "*", as for FASTA input / -q queries). */
+ * qual may be NULL: no read has a quality (SAM QUAL "*", as for FASTA input / -q queries).
+ * qual_null (optional, may be NULL) marks single reads without one, one byte per read: nonzero =
+ * read i's Read.getQual(0) is null (R/SingleEndRead.java:74-76, FASTA records) and its QUAL prints
+ * "*" (R/AlignmentRecord.java:157) -- its qual_off range is ignored.  Zero-initialise the struct. */
 typedef struct {
   uint32_t n;
   const char *name, *seq, *qual;
   const uint64_t *name_off, *seq_off, *qual_off;
+  const uint8_t *qual_null;
 } gwa_reads_t;
 
 /* Reads parsed by the library from FASTA / FASTQ text (gwa_reads_parse); `reads` points into
@@ -77,7 +81,8 @@ typedef struct {
 
 /* Library-owned SAM text (no header), in input order; read i's lines are
  * sam[line_off[i], line_off[i+1]).  Free with gwa_results_free.  records / n_records are filled on
- * request by gwa_results_records (NULL / 0 until then). */
+ * request by gwa_results_records (NULL / 0 until then).  paired = 1: results of a paired-end batch,
+ * unit i = pair i, two mate lines (mate 1, mate 2), never split records. */
 typedef struct {
   uint32_t n_reads;
   char *sam;
@@ -85,6 +90,7 @@ typedef struct {
   uint64_t *line_off; /* n_reads + 1 */
   gwa_record_t *records;
   uint64_t n_records;
+  uint32_t paired;
 } gwa_results_t;
 
 /* Per-batch counters (instrumentation for SURVEY.md §8d roofline accounting). */
@@ -191,8 +197,11 @@ int gwa_batch_read_counters(gwa_batch_t *b, int32_t *out);
  * to them as they become free (workers_per_device host threads per handle overlap one batch's set-up
  * and SAM formatting with another's kernels).  Output is in input order, byte-identical to a
  * single-handle run.  The handles must outlive the pipeline.  workers_per_device <= 0 means 3.
- * gwa_pipeline_open pins the read-text buffers a file run keeps in flight (about 5.4 GB for one
- * device, roughly a second); they and each worker's pinned SAM buffer are kept for later calls. */
+ * The first gwa_pipeline_align_file call pins the read-text buffers a file run keeps in flight (sized
+ * from the file, at most a quarter of the host's available memory; about 5.4 GB for a large file on
+ * one device); they and each worker's pinned SAM buffer are kept for later calls.  In-memory runs
+ * (gwa_pipeline_align) pin nothing.  Output to an O_APPEND descriptor or a pipe is written in batch
+ * order with write(); to a regular file, each batch at its offset with pwrite(). */
 typedef struct gwa_pipeline gwa_pipeline_t;
 typedef struct {
   uint64_t reads, batches;

@@ -13,6 +13,7 @@
 #include "../../genome-weaver-align_amd/csrc/host_index.h"
 #include "../../genome-weaver-align_amd/csrc/sam.h"
 #include "../../genome-weaver-align_amd/csrc/sam_core.h"
+#include "../../genome-weaver-align_amd/csrc/text_core.h"
 
 using namespace gwa;
 
@@ -97,7 +98,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
     const char *qv = quals ? quals[i] : nullptr;
     const uint64_t nameOff[2] = {0, strlen(names[i])}, qualOff[2] = {0, qv ? strlen(qv) : 0};
     const uint32_t codeOff[1] = {0}, codeLen[1] = {(uint32_t)mlen};
-    const SamText t{names[i], nameOff, nameOff + 1, qv, qualOff, qualOff + 1, codes.data(), codeOff, codeLen,
+    const SamText t{names[i], nameOff, nameOff + 1, qv, qualOff, qualOff + 1, nullptr, codes.data(), codeOff, codeLen,
                     sn.blob.data(), sn.off.data(), rk.data(), sn.starKey, sn.emptyKey};
     if (hd.status == ST_MAPPED || hd.status == ST_UNMAPPED) {
       SamOut cnt{nullptr, 0};
@@ -205,3 +206,6 @@ int hc_align(void *p, float k, int reportType, int numSplit, int strategy, uint3
   return 0;
 }
 }
+
+// the encode kernels' byte-parallel ACGT.to3bitCode (text_core.h)
+extern "C" uint32_t hc_to3bit4(uint32_t x) { return to3bit4(x); }

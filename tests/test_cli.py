@@ -85,7 +85,8 @@ def _native_records(text, fmt, chunk):
 FASTA_CASES = [b">r1 desc\nACGT\n  AC GT \r\n>r2\r\nNNNN\r>  \nAC\n", b"junk\n>a\n\nAC\n\n>b x y\nG", b"",
                b">only\n", b">\t t\x0bz\nac\x1cgt\n\n", b"no header\nat all\n"]
 FASTQ_CASES = [b"@a x\nACGT\n+\nIIII\n\n@b\r\nAC\r\n+b\r\nII\r\n", b"\n\n@r\nA\n+\nI", b"",
-               b"@\tq1\x0c extra\nACGN\n+q1\n!!!!\n@q2\n\n+\n\n"]
+               b"@\tq1\x0c extra\nACGN\n+q1\n!!!!\n@q2\n\n+\n\n",
+               b"@c1\rACGT\r+\rIIII\r@c2 x\rGG\r+\r!!\r"]  # "\r" line ends only
 
 
 @pytest.mark.parametrize("i", range(len(FASTA_CASES)))
@@ -102,6 +103,21 @@ def test_native_fastq_parser_matches_python(i):
     exp = _py_records(t, "fastq")
     for chunk in range(1, len(t) + 2):
         assert _native_records(t, "fastq", chunk) == exp, chunk
+
+
+def test_native_parser_cr_only_text_is_linear():
+    # FASTQ with "\r" line ends only: the line scanner stops at the first "\r" of a bounded window
+    # instead of searching to the end of the text for a "\n" on every line (quadratic before)
+    import time
+    rec = b"@r%d\r" + b"ACGT" * 25 + b"\r+\r" + b"I" * 100 + b"\r"
+    t = b"".join(rec % k for k in range(40000))  # 8.6 MB, 160k lines
+    t0 = time.perf_counter()
+    pr = gwa.ParsedReads(t, "fastq", True)
+    dt = time.perf_counter() - t0
+    assert pr.n == 40000 and pr.consumed == len(t)
+    assert pr.records()[123] == ("r123", "ACGT" * 25, "I" * 100)
+    pr.close()
+    assert dt < 2.0, dt
 
 
 def test_native_parser_fixtures_and_errors():
@@ -255,3 +271,27 @@ def test_cli_paired_end_files(tmp_path):
     assert gwa_cli.align(ns, out=out) == 600
     oi = O.Index.from_fasta(ref.read_text())
     assert out.getvalue() == oi.sam_header() + oi.align_pairs(r1, r2, O.OrcConfig.default(k=2.0))
+
+
+@pytest.mark.gpu
+def test_pipeline_appends_in_input_order(tmp_path):
+    # an O_APPEND descriptor (shell ">>", open(..., "a")): pwrite would ignore the batch offsets and
+    # append in completion order, so such output takes the in-order write path; several workers
+    # over two handles and small batches give the same bytes as the oracle, after the old content
+    import oracle as O
+    ref, rp, reads = _e2e_inputs(tmp_path, "fq", n=2500, cid=17)
+    fm = gwa.FMIndexOnGenome.load(str(ref))
+    fm2 = gwa.FMIndexOnGenome.load(str(ref))
+    out = tmp_path / "out.sam"
+    out.write_bytes(b"@HD\tVN:1.0\n")
+    pipe = gwa.Pipeline([fm, fm2], gwa.AlignmentConfig(k=2.0), batch_reads=61, workers_per_device=4)
+    with open(out, "ab") as f:
+        assert pipe.align_file(str(rp), f.fileno()) == len(reads)
+    with open(out, "ab") as f:  # and once more: appended after the first run's records
+        assert pipe.align_file(str(rp), f.fileno()) == len(reads)
+    pipe.close()
+    fm.close()
+    fm2.close()
+    oi = O.Index.from_fasta(ref.read_text())
+    sam = oi.align(reads, O.OrcConfig.default(k=2.0))
+    assert out.read_text() == "@HD\tVN:1.0\n" + sam + sam

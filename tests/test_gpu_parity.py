@@ -136,8 +136,10 @@ def test_edge_reads(random_pair):
         reads.append(("n%d" % i, "".join(s), "I" * 100))
     reads += [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), None) for i in range(100)]
     reads += [("short", "ACG", None), ("lower", strs[0].lower(), None), ("u", strs[1].replace("T", "U"), None)]
-    # a batch must have quals for all or none
+    # reads with and without a quality in one batch (FASTA reads have none: QUAL "*", per read)
+    _check(gi, oi, reads, k=2.0)
     _check(gi, oi, [(a, b, c if c else "I" * len(b)) for a, b, c in reads], k=2.0)
+    _check(gi, oi, [(a, b, None) for a, b, c in reads], k=2.0)
 
 
 def test_reads_longer_than_255_fail_at_batch_creation(random_pair, gwa):
@@ -223,7 +225,7 @@ def test_sf_edge_reads(random_pair):
             s[j] = "N"
         reads.append(("n%d" % i, "".join(s), "I" * 100))
     reads += [("x%d" % i, "".join(rng.choice(list("ACGT"), 100)), "I" * 100) for i in range(100)]
-    reads += [("short", "ACG", "III"), ("lower", strs[0].lower(), "I" * 100)]
+    reads += [("short", "ACG", "III"), ("lower", strs[0].lower(), "I" * 100), ("noqual", strs[2], None)]
     _check(gi, oi, reads, k=2.0, strategy="sf")
 
 
@@ -465,6 +467,35 @@ def test_paired_end_insert_window_and_unmapped_mates(random_pair):
     r2 = [(n, "".join(rng.choice(list("ACGT"), 100)) if i % 7 == 0 else s, q) for i, (n, s, q) in enumerate(r2)]
     got = gwa.PairedEndAligner(gi, gwa.AlignmentConfig(k=2.0), 295, 305).align_pairs(r1, r2)
     assert got == oi.align_pairs(r1, r2, O.OrcConfig.default(k=2.0), 295, 305)
+    # mate 2 without qualities (a FASTA mate file) and single mate-1 reads without one
+    r1q = [(n, s, None if i % 5 == 0 else q) for i, (n, s, q) in enumerate(r1)]
+    r2q = [(n, s, None) for n, s, q in r2]
+    got = gwa.PairedEndAligner(gi, gwa.AlignmentConfig(k=2.0)).align_pairs(r1q, r2q)
+    assert got == oi.align_pairs(r1q, r2q, O.OrcConfig.default(k=2.0))
+
+
+def test_results_records_of_a_paired_batch(random_pair):
+    # gwa_results_records on paired-end results: two mate lines per pair, each its own record (no
+    # split linking: FLAG 0x41 / 0x81 are mates here, not a split record pair)
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    m1, m2 = synth.pairs_codes(codes, lengths, 300, config_id=54)
+    off = np.arange(0, 100 * 301, 100, dtype=np.uint64)
+    nb, no = synth.name_blob(300)
+    s1, s2 = synth.SYM[m1].tobytes(), synth.SYM[m2].tobytes()
+    b = gwa.Batch(gi, gwa.AlignmentConfig(k=2.0), pair_blobs=((nb, no, s1, off, b"I" * 30000, off),
+                                                              (nb, no, s2, off, b"J" * 30000, off)))
+    b.run()
+    sam, recs = b.records(gi)
+    b.close()
+    lines = sam.splitlines()
+    assert len(recs) == len(lines) == 600
+    assert all(r.split == -1 and r.is_split == 0 for r in recs)
+    assert [r.read for r in recs] == [i // 2 for i in range(600)]
+    assert all((r.flag & 0x40) if i % 2 == 0 else (r.flag & 0x80) for i, r in enumerate(recs))
+    for r, line in zip(recs, lines):
+        f = line.split("\t")
+        assert r.pos == int(f[3]) and r.flag == int(f[1])
 
 
 def test_gpu_cyclic_sa_known_answers(gwa):

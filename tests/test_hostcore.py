@@ -233,3 +233,20 @@ def test_dp_slice_fallback(random_genome, repetitive_genome, monkeypatch, strate
     _cmp(codes, names, lengths, [(rn[i], strs[i], None) for i in range(len(strs))], 5.0, strategy=strategy)
     codes, names, lengths = repetitive_genome
     _cmp(codes, names, lengths, _mk(codes, 150, 100, 2, True, seed=5), 2.0, strategy=strategy)
+
+
+def test_byte_parallel_to3bit_matches_acgt_table():
+    # text_core.h to3bit4 (the encode kernels: four text bytes per word) against ACGT.to3bitCode
+    # (A/ACGT.java:36-43) for every byte value in every byte lane
+    import ctypes
+    from hostcore import lib as hlib
+    L = hlib()
+    L.hc_to3bit4.restype = ctypes.c_uint32
+    L.hc_to3bit4.argtypes = [ctypes.c_uint32]
+    table = {ord(c): v for c, v in zip("AaCcGgTtUu", [0, 0, 1, 1, 2, 2, 3, 3, 3, 3])}
+    for b in range(256):
+        for lane in range(4):
+            x = (b << (8 * lane)) | (ord("G") << (8 * ((lane + 1) % 4)))
+            got = L.hc_to3bit4(x)
+            assert (got >> (8 * lane)) & 0xFF == table.get(b, 4), (b, lane)
+            assert (got >> (8 * ((lane + 1) % 4))) & 0xFF == 2

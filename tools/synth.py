@@ -211,14 +211,18 @@ def reads_codes(codes, lengths, n, m=100, max_subs=2, config_id=2, shard=0, inde
         c = min(chunk, n - c0)
         ci = rng.choice(len(L), size=c, p=p)
         starts = offs[ci] + (rng.random(c) * (L[ci] - m - 1)).astype(np.int64)
-        # start uniform over N-free windows: redraw the windows that hold an N
+        # start uniform over N-free windows: redraw the windows that hold an N (only redrawn windows
+        # are checked again: the others are unchanged, so the draws are those of a full re-check)
+        W = m + (8 if indels else 0)
+        chk = np.arange(c)
         for _ in range(64):
-            win = codes[np.minimum(starts[:, None] + np.arange(m + (8 if indels else 0))[None, :], N - 1)]
-            bad = np.nonzero((win == 4).any(axis=1))[0]
+            win = codes[np.minimum(starts[chk][:, None] + np.arange(W)[None, :], N - 1)]
+            bad = chk[(win == 4).any(axis=1)]
             if len(bad) == 0:
                 break
             cj = rng.choice(len(L), size=len(bad), p=p)
             starts[bad] = offs[cj] + (rng.random(len(bad)) * (L[cj] - m - 1)).astype(np.int64)
+            chk = bad
         if not indels:
             idx = starts[:, None] + np.arange(m)[None, :]
             blk = codes[np.minimum(idx, N - 1)]
