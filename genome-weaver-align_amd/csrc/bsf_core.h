@@ -1678,7 +1678,8 @@ struct BsfLane {
     ru = ru > ix.N ? ix.N : ru;
     uint64_t w2 = 0, wN = 0;
     Block B0, B1;
-    if (kind == K_TEXT && !tcOn) {
+    const int tc = tcOn | cfg.textCache;  // text words through the lane's one-word cache (refCodeCached)
+    if (kind == K_TEXT && !tc) {
       w2 = ix.text2[p >> 5];
       wN = ix.textN[p >> 6];
     }
@@ -1693,7 +1694,7 @@ struct BsfLane {
       d.meta |= M_TEXT | (hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD);
       d.lb[0] = (uint32_t)t;
       d.lb[1] = (uint32_t)len;
-      d.lb[2] = (uint32_t)(tcOn ? refCodeCached(p) : ((wN >> (p & 63)) & 1) ? 4 : (int)((w2 >> ((p & 31) * 2)) & 3));
+      d.lb[2] = (uint32_t)(tc ? refCodeCached(p) : ((wN >> (p & 63)) & 1) ? 4 : (int)((w2 >> ((p & 31) * 2)) & 3));
       d.lb[3] = 0;
       for (int i = 0; i < 4; ++i) d.ub[i] = 0;
       d.bBase = 0;
@@ -1960,14 +1961,20 @@ struct BsfLane {
       xT = tt;
       if (ch >= 0) {
         storeStateWord(xC, xCS.state);
+        GWA_PT(tn);
         int ns = nextStateLocal(xC, xCS, ch);
+        GWA_PA(PR_LOOP, tn);
         if (ns == -2) return SS_DONE;
         if (ns >= 0) {
           if (first && xC == xBase) {
+            GWA_PT(tra);
             ns = runAhead(ns);
+            GWA_PA(PR_BOUND, tra);
             if (ns == -2) return SS_DONE;
           }
+          GWA_PT(tad);
           queueAdd(update(xBase, xC, ns));
+          GWA_PA(PR_ADD1, tad);
           if (first) {
             xMode = 0;
             GWA_PA(PR_EXP1, te);
@@ -2038,7 +2045,11 @@ struct BsfLane {
     // reads are in flight.  Counts and results are those of the reference order.
     bool nfaOk = false;
     GWA_PT(tf);
-    nextSi(cs, ch, d, [&] { nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm); });
+    nextSi(cs, ch, d, [&] {
+      GWA_PT(tq);
+      nfaOk = nfaNext(cs, ch, strand, rows, &nh, &nko, &hm);
+      GWA_PA(PR_NFA, tq);
+    });
     GWA_PA(PR_FM, tf);
     ++numFMIndexSearches;
     tr(2, (uint32_t)ch, d.lb[0] ^ (d.ub[1] * 3u) ^ (d.lb[2] * 7u) ^ (d.ub[3] * 11u) ^ d.bBase, (uint32_t)(d.meta & 3));
@@ -2134,7 +2145,7 @@ struct BsfLane {
     if (!heapNoop(&bound)) return ns;
     // the run works on the register copy `cache` (the state to be polled next) in place
     int moved = 0;
-    tcW2 = tcWN = -1;
+    if (!cfg.textCache) tcW2 = tcWN = -1;
     for (int it = 0; it < cfg.runAheadMax; ++it) {
       // loop top (:352-356) and the poll checks (:358-385) for the cached state
       if (numFMIndexSearches > upperSearches || status == ST_OVERFLOW || status == ST_ERROR) break;
@@ -2194,6 +2205,7 @@ struct BsfLane {
       stairTab = st.tab + (stairBad ? 0 : b);
     }
     quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = textSteps = textRuns = 0;
+    tcW2 = tcWN = -1;
     numSW = verifyBytes = 0;
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains

@@ -529,6 +529,7 @@ static bool batchHead(gwa_index *ix, const gwa_config_t *cfg, uint32_t n, gwa_ba
   sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 14;
   sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
   sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
+  sc.textCache = getenv("GWA_TEXT_CACHE") ? atoi(getenv("GWA_TEXT_CACHE")) : 0;
   HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   return false;
 }
@@ -934,7 +935,7 @@ int gwa_batch_run(gwa_batch_t *b) {
         HIPCHK(hipFree(d_prof));
         double sum[PR_N] = {};
         for (size_t i = 0; i < pv.size(); ++i) sum[i % PR_N] += (double)pv[i];
-        static const char *nm[PR_N] = {"poll", "report", "bound", "exp1", "add1", "expN", "split", "loop",
+        static const char *nm[PR_N] = {"poll", "report", "runahead", "exp1", "add1", "expN", "split", "newstate",
                                        "verify", "nfa", "fm", "seed", "nVerifyWave", "nVerifyLane", "nStepWave",
                                        "nStepLane", "dpFwd", "dpTrace", "sumWait", "wave"};
         fprintf(stderr, "[gwa-prof] tier %d reads %u lanes %u (Gcycles summed over waves; counts in M):", t, n, lanes);

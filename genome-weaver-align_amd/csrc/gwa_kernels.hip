@@ -177,7 +177,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
     if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_NWAIT] += (uint64_t)nWait;
 #endif
     if (nWait > 0 && nWait * 16 >= cfg.waitQ16 * (nWait + nRun)) {
+#ifdef GWA_PROF
+      const uint64_t trp = clock64();
+#endif
       if (phase == WAIT) phase = lane.searchReport() ? RUN : FINISH;
+#ifdef GWA_PROF
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_REPORT] += clock64() - trp;
+#endif
     } else if (phase == RUN) {
       const int sst = lane.searchStep();
       phase = sst == BsfLane<R, QW>::SS_REPORT ? WAIT : sst == BsfLane<R, QW>::SS_DONE ? FINISH : RUN;

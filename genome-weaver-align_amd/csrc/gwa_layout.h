@@ -79,6 +79,9 @@ struct SearchConfig {
   // BsfLane::runAhead: at most this many text-mode match steps run back to back per search step
   // (0 = off).  A lane running ahead holds its wavefront, so long runs cost the other lanes time.
   int32_t runAheadMax;
+  // 1: every text-mode FM step reads the text through the lane's one-word cache (BsfLane::refCodeCached),
+  // kept across search steps (the states of one read mostly walk one text neighbourhood)
+  int32_t textCache;
 };
 
 // Read batch as resident in HBM: one byte code (0..4) per base; every read starts at a 16-B

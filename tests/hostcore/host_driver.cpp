@@ -175,6 +175,7 @@ int hc_align(void *p, float k, int reportType, int numSplit, int strategy, uint3
   cfg.waitQ16 = 16;
   cfg.textSearch = (numSplit <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;  // as gwa_batch_create
   cfg.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 1000;  // long runs on the CPU
+  cfg.textCache = getenv("GWA_TEXT_CACHE") ? atoi(getenv("GWA_TEXT_CACHE")) : 1;
   std::vector<int> lens;
   int kmax = 0;
   for (uint32_t i = 0; i < n; ++i) {

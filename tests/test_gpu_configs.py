@@ -1,7 +1,8 @@
 """Every BASELINE.json config as a GPU parity test at its own scale.
 
-- C2 / C4 on the FULL-SIZE hg19-like genome (tools/synth.genome_repeats at hg19 contig lengths:
-  3.1 Gbp with N gaps, repeat families, satellites and segmental duplications): a large batch runs
+- C2 / C4 on the FULL-SIZE hg19-like genome (here: tools/synth.genome_repeats at hg19 contig lengths,
+  3.1 Gbp with N gaps, repeat families, satellites and segmental duplications) and on the full-size
+  hg19 stand-in with N gaps (test_gpu_configs_hg19.py): a large batch runs
   on the GPU; the SAM of a random sample plus EVERY read that needed a search tier >= 1 is compared
   byte for byte with the oracle.  The oracle index takes the GPU suffix arrays only after the
   complete O(n) check of both (oracle/ orc_check_cyclic_sa_full: permutation + every adjacent pair),
@@ -113,14 +114,16 @@ def test_c2_full_size_hg19r_k2(hg19r_full, request):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("strategy", ["bsf", "sf"])
-def test_c4_full_size_hg19r_indels_k5(hg19r_full, request, strategy):
+def test_c4_full_size_hg19r_indels_k5(hg19r_full, request):
     """C4: 150 bp, 0-5 edits (60 % substitutions, 20 % 1-bp insertions, 20 % 1-bp deletions), -k 5,
-    on the full-size hg19-like genome: 100k reads on the GPU, 50k random + every tier >= 1 read."""
+    -m bsf on the full-size hg19-like genome: 100k reads on the GPU, 50k random + every tier >= 1
+    read.  (-m sf at this scale: test_gpu_configs_hg19.py -- on the full-size repeat families the
+    reference's SuffixFilter search is unbounded, S/SuffixFilter.java:257-290, and some reads grow past
+    any state budget)"""
     codes, names, lengths, gi, oi = hg19r_full
     strs = synth.to_strings(synth.reads_codes(codes, lengths, 100_000, 150, 2, config_id=4, indels=True,
                                               max_edits=5))
-    _batch_and_check(request, gi, oi, strs, 150, 5.0, strategy, 50_000)
+    _batch_and_check(request, gi, oi, strs, 150, 5.0, "bsf", 50_000)
 
 
 # ---- C3: reads sharded over processes, one index replica per process ----
