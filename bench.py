@@ -198,6 +198,66 @@ def make_reads(synth, np, codes, lengths, n, m, c4, rank):
     return (name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off)
 
 
+def write_fastq(np, path, name_blob, seq_blob, n, m):
+    """reads as a FASTQ file: "@r%09d\n" seq "\n+\n" qual "\n" """
+    rec = np.empty((n, 12 + m + 3 + m + 1), dtype=np.uint8)
+    rec[:, 0] = ord("@")
+    rec[:, 1:11] = np.frombuffer(name_blob, dtype=np.uint8).reshape(n, 10)
+    rec[:, 11] = ord("\n")
+    rec[:, 12:12 + m] = np.frombuffer(seq_blob, dtype=np.uint8).reshape(n, m)
+    rec[:, 12 + m:15 + m] = np.frombuffer(b"\n+\n", dtype=np.uint8)
+    rec[:, 15 + m:15 + 2 * m] = ord("I")
+    rec[:, 15 + 2 * m] = ord("\n")
+    with open(path, "wb") as f:
+        f.write(rec.data)
+
+
+def host_ceiling_leg(args, gwa, synth, np, log, handles=4):
+    """detail.host_ceiling: what the host side of gwa_pipeline_align_file (read, frame, H2D, D2H of the
+    SAM text, ordered writes) sustains when the devices are not the limit: 10M exact 100 bp reads of an
+    E. coli-size genome (-k 0: the quick scan ends every read, so the kernels take a few ms per batch and
+    the SAM lines are C2-sized) through `handles` index replicas on this GPU, 3 workers each.  The
+    C2 device rate times the GPU count a node needs is to be compared with it."""
+    import tempfile
+    n, m = 10_000_000, 100
+    codes, names, lengths = synth.genome(synth.ECOLI, config_id=1)
+    seqs = synth.reads_codes(codes, lengths, n, m, 0, config_id=11)
+    seq_blob = synth.SYM[seqs].tobytes()
+    del seqs
+    name_blob, _ = synth.name_blob(n)
+    d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+    fq, so = os.path.join(d, "reads.fq"), os.path.join(d, "out.sam")
+    write_fastq(np, fq, name_blob, seq_blob, n, m)
+    del seq_blob, name_blob
+    gis = [gwa.FMIndexOnGenome.buildFromCodes(codes, names, lengths) for _ in range(handles)]
+    pipe = gwa.Pipeline(gis, gwa.AlignmentConfig(k=0.0), workers_per_device=3)
+    legs = []
+    for _ in range(2):
+        with open(so, "wb") as f:
+            t0 = time.perf_counter()
+            got = pipe.align_file(fq, f.fileno())
+            legs.append(time.perf_counter() - t0)
+    pst = pipe.stats()
+    sam_bytes = os.path.getsize(so)
+    pipe.close()
+    for g in gis:
+        g.close()
+    for x in (fq, so):
+        os.remove(x)
+    os.rmdir(d)
+    T, tdesc = host_cores()
+    out = {"reads_per_s": got / legs[1], "seconds": legs[1], "first_pass_seconds": legs[0], "reads": got,
+           "handles": handles, "workers": 3 * handles, "host_cores": T, "sam_bytes": sam_bytes,
+           "sam_GBps": sam_bytes / legs[1] / 1e9, "fastq_GBps": got * (2 * m + 15) / legs[1] / 1e9,
+           "stages_s": {"read": pst.read_s, "frame": pst.frame_s, "setup": pst.setup_s,
+                        "kernels": sum(pst.device_kernel_s[:handles]), "sam_format_d2h": pst.format_s,
+                        "write": pst.write_s, "order_wait": pst.order_wait_s},
+           "note": "FASTQ file -> SAM file through gwa_pipeline_align_file with %d index replicas (E. coli-size, "
+                   "-k 0, exact reads) on one GPU: the host side's ceiling on %s; second pass" % (handles, tdesc)}
+    log("host ceiling: %.1f M reads/s (%d handles, %.1f GB/s SAM out)" % (out["reads_per_s"] / 1e6, handles, out["sam_GBps"]))
+    return out
+
+
 def hg19r_leg(args, gen, gwa, synth, np, cfg, log):
     """detail.hg19r: the same C2 step on the hg19-like repetitive genome (tools/synth.genome_repeats,
     generated by a child process while the main leg ran)."""
@@ -282,8 +342,11 @@ def main():
 
     dist = world > 1
     if dist:
+        import torch
         import torch.distributed as tdist
-        tdist.init_process_group("gloo")
+        # CPU tensors (timings, barriers) over gloo; the optional SAM gather of device buffers over RCCL
+        # (nccl) when every rank has a GPU of its own (torch.cuda.device_count does not initialise the GPU)
+        tdist.init_process_group("cpu:gloo,cuda:nccl" if torch.cuda.device_count() >= world else "gloo")
     import torch
     dev = gdist.device_for(local, torch.cuda.device_count())
     torch.cuda.set_device(dev)
@@ -330,12 +393,37 @@ def main():
         return (name_blob[10 * i:10 * i + 10].decode(), seq_blob[m * i:m * i + m].decode(), "I" * m)
 
     def barrier():
-        if dist:
-            tdist.barrier()
+        if dist:  # a CPU all-reduce (gloo), whatever the device backend
+            tdist.all_reduce(torch.zeros(1))
 
     mine, window, kms, st, sam_bytes = timed_steps(batch, args.steps, args.warmup, barrier)
     rank_times = gdist.all_gather_floats(mine)
     dt = max(rank_times)
+
+    # SURVEY.md §8e's optional collective, outside the timed region: the SAM text of the last step, in
+    # HBM on every rank, gathered in rank order (= input order) over RCCL / xGMI
+    gather = None
+    if dist and torch.cuda.device_count() >= world:
+        try:
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            merged = gdist.gather_sam_device(batch.sam_device())
+            torch.cuda.synchronize()
+            tg = time.perf_counter() - t0
+            tot = gdist.all_gather_floats(float(sam_bytes))
+            gather = {"seconds": tg, "bytes_per_rank": tot, "backend": "nccl (RCCL)",
+                      "merged_bytes": int(merged.numel()) if merged is not None else None,
+                      "GBps_gathered": sum(tot) / tg / 1e9 if tg > 0 else None,
+                      "note": "all-gather of the lengths, then of the texts padded to the longest; rank 0 keeps "
+                              "the concatenation in rank order"}
+            if merged is not None and int(merged.numel()) != int(sum(tot)):
+                gather["error"] = "merged size differs from the sum of the ranks' SAM sizes"
+            del merged
+        except Exception as e:  # reported, never fatal to the timing
+            gather = {"error": repr(e)}
+    elif dist:
+        gather = {"skipped": "ranks share a GPU (RCCL needs one GPU per rank)"}
 
     # host pipeline (first bullet): the whole path for one batch outside the timed
     # region -- reads from host memory to HBM (batch create), kernels, SAM text to the host -- reported
@@ -365,17 +453,7 @@ def main():
         d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
         fq, so = os.path.join(d, "reads.fq"), os.path.join(d, "out.sam")
         t0 = time.perf_counter()
-        rec = np.empty((reads_per_step, 12 + m + 3 + m + 1), dtype=np.uint8)  # "@r%09d\n" seq "\n+\n" qual "\n"
-        rec[:, 0] = ord("@")
-        rec[:, 1:11] = np.frombuffer(name_blob, dtype=np.uint8).reshape(reads_per_step, 10)
-        rec[:, 11] = ord("\n")
-        rec[:, 12:12 + m] = np.frombuffer(seq_blob, dtype=np.uint8).reshape(reads_per_step, m)
-        rec[:, 12 + m:15 + m] = np.frombuffer(b"\n+\n", dtype=np.uint8)
-        rec[:, 15 + m:15 + 2 * m] = ord("I")
-        rec[:, 15 + 2 * m] = ord("\n")
-        with open(fq, "wb") as f:
-            f.write(rec.data)
-        del rec
+        write_fastq(np, fq, name_blob, seq_blob, reads_per_step, m)
         t_write = time.perf_counter() - t0
         # two passes over the file on one pipeline: the first also pins the pipeline's host buffers,
         # the second is the steady state
@@ -404,6 +482,10 @@ def main():
         for x in (fq, so):
             os.remove(x)
         os.rmdir(d)
+
+    hostc = None
+    if rank == 0 and world == 1 and not args.no_pipeline and not c4:
+        hostc = host_ceiling_leg(args, gwa, synth, np, log)
 
     counters = batch.read_counters()  # also fetches the records (stats below)
     st = batch.stats()
@@ -512,7 +594,8 @@ def main():
                                    "traffic": _pmc_traffic("fm_quickscan", workload)[0],
                                    "gather_ceiling": gather_ceiling(st, q_ms)},
                    "mapped": st.n_mapped, "unmapped": st.n_unmapped, "index_build_s": t_index,
-                   "index_gb": index_gb, "parity": parity, "hg19r": hg},
+                   "index_gb": index_gb, "parity": parity, "hg19r": hg, "host_ceiling": hostc,
+                   "sam_gather": gather},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -556,7 +639,7 @@ def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_i
         batch.run()
         batch.format_device()
     if dist:
-        tdist.barrier()
+        tdist.all_reduce(torch.zeros(1))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     win0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
@@ -570,7 +653,7 @@ def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_i
         batch.format_device()
     torch.cuda.synchronize()
     if dist:
-        tdist.barrier()
+        tdist.all_reduce(torch.zeros(1))
     win1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     rank_times = gdist.all_gather_floats(time.perf_counter() - t0)
     dt = max(rank_times)

@@ -213,9 +213,13 @@ struct LaneMem {
   uint32_t oPath;          // byte offset of the path plane in the chunk
   int lane, is;            // lane in the interleaved block, interleave stride (elements)
   // PriorityQueue array of (key << 16 | state index): entry i at heapP[i * hs].  In the slice
-  // (hs = 1) or, for the first tier, in LDS interleaved across the workgroup (hs = 256)
+  // (hs = 1) or, for the first tier, in LDS interleaved across the workgroup (hs = 256).
+  // Hybrid heap (BsfLane::kHybridHeap, k >= 4 kernels): entries [0, heapH) in LDS at heapL[i * 256],
+  // the rest in the slice at heapG[i] (heapH = 0: all in the slice)
   uint64_t *heapP;
   int hs;
+  uint64_t *heapL = nullptr, *heapG = nullptr;
+  int heapH = 0;
   GWA_HD DState<R> *arena() const { return (DState<R> *)slice; }
   GWA_HD uint64_t *heap() const { return heapP; }
   GWA_HD int64_t *cand() const { return (int64_t *)(slice + oCand); }
@@ -259,6 +263,8 @@ GWA_HD LaneMem<R> laneMem(uint8_t *slice, uint8_t *chunk, int laneInWave, int is
   L.is = is;
   L.heapP = (uint64_t *)(slice + L.oHeap);
   L.hs = 1;
+  L.heapG = L.heapP;
+  L.heapH = 0;
   return L;
 }
 template <int R>
@@ -344,8 +350,8 @@ struct RefWindow {
 struct Overflow {};  // thrown only on host test builds; device uses status codes
 
 // QW = 2-bit query words per strand held in registers (4: reads <= 128 bp, 8: <= 255 bp); the
-// DP then needs at most DB = QW / 2 blocks of 64 rows.
-template <int R, int QW = 8>
+// DP then needs at most DB = QW / 2 blocks of 64 rows.  HY: hybrid heap (hslot).
+template <int R, int QW = 8, bool HY = false>
 struct BsfLane {
   static constexpr int DB = QW / 2;
   const IndexView &ix;
@@ -794,10 +800,17 @@ struct BsfLane {
     const int proc = cProcessed(S(s));
     return ((uint64_t)pr << 40) | (sp << 8) | (uint64_t)(255 - proc);
   }
+  // Heap slot i: the LDS / slice array of the kernel instance (first tier: LDS), or, with the hybrid
+  // heap (HY; k >= 4 kernels: their heaps outgrow a small LDS array, deep heaps are rare), LDS for the
+  // top slots and the slice beyond them -- one flat address either way
+  GWA_HD uint64_t &hslot(int i) const {
+    if (HY) return i < L.heapH ? L.heapL[(size_t)i * 256] : L.heapG[i];
+    return L.heap()[(size_t)i * L.hs];
+  }
   GWA_HD void refreshKeys() {
     for (int i = 0; i < heapSize; ++i) {
-      const int idx = (int)(L.heap()[(size_t)(i) * L.hs] & 0xFFFF);
-      L.heap()[(size_t)(i) * L.hs] = (keyOf(idx) << 16) | (uint64_t)idx;
+      const int idx = (int)(hslot(i) & 0xFFFF);
+      hslot(i) = (keyOf(idx) << 16) | (uint64_t)idx;
     }
   }
   // java.util.PriorityQueue.offer / poll on cached keys.  The element moves are exactly Java's
@@ -820,7 +833,7 @@ struct BsfLane {
       for (int d = 0; d < MAXD; ++d) {
         const int p = idx > 0 ? (idx - 1) >> 1 : 0;
         ai[d] = p;
-        av[d] = L.heap()[(size_t)(p) * L.hs];
+        av[d] = hslot(p);
         idx = p;
       }
     }
@@ -833,25 +846,25 @@ struct BsfLane {
     for (int d = MAXD - 1; d >= 0; --d) t = (d >= depth || ek >= (av[d] >> 16)) ? d : t;
 #pragma unroll
     for (int d = 0; d < MAXD; ++d)
-      if (d < t) L.heap()[(size_t)(d == 0 ? kk : ai[d - 1]) * L.hs] = av[d];
+      if (d < t) hslot(d == 0 ? kk : ai[d - 1]) = av[d];
     int pos = t == 0 ? kk : pick(ai, t - 1);
     if (t == MAXD) {  // deeper than MAXD levels (large tiers only): Java's loop from there
       while (pos > 0) {
         const int parent = (pos - 1) >> 1;
-        const uint64_t p = L.heap()[(size_t)(parent) * L.hs];
+        const uint64_t p = hslot(parent);
         if (ek >= (p >> 16)) break;
-        L.heap()[(size_t)(pos) * L.hs] = p;
+        hslot(pos) = p;
         pos = parent;
       }
     }
-    L.heap()[(size_t)(pos) * L.hs] = e;
+    hslot(pos) = e;
     tr(9, (uint32_t)(e & 0xFFFF), (uint32_t)kk, (uint32_t)pos);
   }
   GWA_HD int queuePoll() {
     if (heapSize == 0) return -1;
     int s = --heapSize;
-    const uint64_t result = L.heap()[(size_t)(0) * L.hs];
-    const uint64_t x = L.heap()[(size_t)(s) * L.hs];
+    const uint64_t result = hslot(0);
+    const uint64_t x = hslot(s);
     if (s != 0) {
       const int n = heapSize, half = n >> 1, capm1 = caps.heap - 1;
       int kk = 0;
@@ -862,16 +875,16 @@ struct BsfLane {
         // at or past n are never selected)
         const int c = (kk << 1) + 1;
         const int g = (kk << 2) + 3;
-        const uint64_t c0 = L.heap()[(size_t)(c) * L.hs], c1 = L.heap()[(size_t)(c + 1 <= capm1 ? c + 1 : capm1) * L.hs];
-        const uint64_t g0 = L.heap()[(size_t)(g <= capm1 ? g : capm1) * L.hs], g1 = L.heap()[(size_t)(g + 1 <= capm1 ? g + 1 : capm1) * L.hs];
-        const uint64_t g2 = L.heap()[(size_t)(g + 2 <= capm1 ? g + 2 : capm1) * L.hs], g3 = L.heap()[(size_t)(g + 3 <= capm1 ? g + 3 : capm1) * L.hs];
+        const uint64_t c0 = hslot(c), c1 = hslot(c + 1 <= capm1 ? c + 1 : capm1);
+        const uint64_t g0 = hslot(g <= capm1 ? g : capm1), g1 = hslot(g + 1 <= capm1 ? g + 1 : capm1);
+        const uint64_t g2 = hslot(g + 2 <= capm1 ? g + 2 : capm1), g3 = hslot(g + 3 <= capm1 ? g + 3 : capm1);
         // level 1
         const int right = (c + 1 < n && (c0 >> 16) > (c1 >> 16)) ? 1 : 0;
         const uint64_t cv = right ? c1 : c0;
         if (xk <= (cv >> 16)) {
           go = 0;
         } else {
-          L.heap()[(size_t)(kk) * L.hs] = cv;
+          hslot(kk) = cv;
           kk = c + right;
           go = kk < half;
         }
@@ -884,13 +897,13 @@ struct BsfLane {
           if (xk <= (dv >> 16)) {
             go = 0;
           } else {
-            L.heap()[(size_t)(kk) * L.hs] = dv;
+            hslot(kk) = dv;
             kk = c2 + right2;
             go = kk < half;
           }
         }
       }
-      L.heap()[(size_t)(kk) * L.hs] = x;
+      hslot(kk) = x;
     }
     tr(10, (uint32_t)(result & 0xFFFF), (uint32_t)heapSize, (uint32_t)(x & 0xFFFF));
     return (int)(result & 0xFFFF);
@@ -2104,7 +2117,7 @@ struct BsfLane {
   // intermediate states, which nothing references (chain-free, not queued, not reported).  The run
   // stops before any state that the loop would treat otherwise -- report, prune, empty or rejected
   // first child, non-text interval -- and that state is pushed as the reference pushes it.
-  GWA_HD uint64_t heapKeyAt(int i) const { return L.heap()[(size_t)i * L.hs] >> 16; }
+  GWA_HD uint64_t heapKeyAt(int i) const { return hslot(i) >> 16; }
   GWA_HD bool heapNoop(uint64_t *bound) const {
     const int kk = heapSize;
     *bound = ~0ULL;

@@ -107,6 +107,8 @@ struct gwa_batch {
   void *d_fmtTmp = nullptr;
   char *d_fmtText = nullptr;
   size_t fmtCap = 0, fmtTmpBytes = 0, fmtTextCap = 0;
+  uint64_t fmtBytes = 0;  // the text of the last formatting, and whether it was the whole batch
+  bool fmtWhole = false;
   unsigned long long *d_stats = nullptr;
   bool statsDone = false;
   // device encoding of the read text (gwa_batch_run re-encodes every run: the timed path starts
@@ -880,6 +882,10 @@ int gwa_batch_run(gwa_batch_t *b) {
         caps.cigar = (int)tierValue("GWA_TIER_CIGAR", t, (uint32_t)T.cigar);
       }
       caps.cand = T.cand;
+      // k >= 4 (R >= 8): a hybrid heap, its top slots in LDS and the rest in the slice, holding as
+      // many entries as the arena has states (k >= 4 heaps outgrow the 8-slot LDS heap of tier 0)
+      const bool hybrid = !sf && b->R >= 8;
+      if (hybrid) caps.heap = caps.arena;
       const int bMax = std::max(1, (m + 63) / 64);
       const int nref = m + 2 * b->kmax + 2;
       caps.dpWords = 2 * bMax * (nref + 1);
@@ -925,7 +931,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0 || hybrid, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                    ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
                    (uint32_t *)d_prof, -1);
       {
@@ -949,7 +955,7 @@ int gwa_batch_run(gwa_batch_t *b) {
                        (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s);
       else
-        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0 || hybrid, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                      ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1],
                      ovfCount, s);
 #endif
@@ -1123,6 +1129,8 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]));
   b->stats.format_ms = ms;
+  b->fmtBytes = total;
+  b->fmtWhole = false;
   return total;
 }
 
@@ -1206,6 +1214,23 @@ int gwa_batch_stats(gwa_batch_t *b, gwa_batch_stats_t *st) {
 int gwa_batch_format(gwa_batch_t *b, uint64_t *sam_bytes) {
   try {
     *sam_bytes = b->headerOnly ? 0 : formatOnDevice(b, nullptr, 0, b->pairs ? b->pairs : b->n);
+    b->fmtWhole = true;
+    if (b->headerOnly) b->fmtBytes = 0;
+    return 0;
+  } catch (std::exception &e) {
+    return fail(e.what());
+  }
+}
+
+int gwa_batch_sam_copy(gwa_batch_t *b, void *dst, uint64_t *len) {
+  try {
+    if (!b->fmtWhole) throw std::runtime_error("gwa_batch_sam_copy: the batch's SAM text was not formatted by gwa_batch_format");
+    *len = b->fmtBytes;
+    if (dst && b->fmtBytes) {
+      HIPCHK(hipSetDevice(b->ix->device));
+      HIPCHK(hipMemcpyAsync(dst, b->d_fmtText, b->fmtBytes, hipMemcpyDeviceToDevice, b->stream));
+      HIPCHK(hipStreamSynchronize(b->stream));
+    }
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());

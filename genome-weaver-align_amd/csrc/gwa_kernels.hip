@@ -83,6 +83,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   if (LH) {
     L.heapP = heapLds + threadIdx.x;
     L.hs = 256;
+    L.heapL = heapLds + threadIdx.x;  // hybrid heap (k >= 4): LDS for the top slots, the slice beyond
+    L.heapH = kLdsHeap;
   }
 #ifdef GWA_PROF
   // profiling build: `trace` is a [lanes][PR_N] cycle-counter array, slot PR_N-1 = wave lifetime
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
         r = list[i];
         const uint32_t o = reads.off[r];
         const int m = (int)reads.len[r];
-        BsfLane<R, QW> lane(ix, cfg, st, L, caps);
+        BsfLane<R, QW, (LH != 0 && R >= 8)> lane(ix, cfg, st, L, caps);
         lane.chrRank = chrRank;
         if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
         __shared__ uint64_t qwLds1[2 * QW * 256];
@@ -124,7 +126,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
     return;
   }
 #endif
-  BsfLane<R, QW> lane(ix, cfg, st, L, caps);
+  typedef BsfLane<R, QW, (LH != 0 && R >= 8)> Lane;  // hybrid heap: k >= 4 kernels with the LDS heap
+  Lane lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
   if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
   __shared__ uint64_t qwLds[2 * QW * 256];  // the lanes' 2-bit read words (BsfLane::qword)
@@ -186,7 +189,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 #endif
     } else if (phase == RUN) {
       const int sst = lane.searchStep();
-      phase = sst == BsfLane<R, QW>::SS_REPORT ? WAIT : sst == BsfLane<R, QW>::SS_DONE ? FINISH : RUN;
+      phase = sst == Lane::SS_REPORT ? WAIT : sst == Lane::SS_DONE ? FINISH : RUN;
     }
     bool ovf = false;
     if (phase == FINISH) {

@@ -62,3 +62,28 @@ def gather_sam(sam_text, dst=0):
     parts = [None] * td.get_world_size() if td.get_rank() == dst else None
     td.gather_object(sam_text, parts, dst=dst)
     return "".join(parts) if td.get_rank() == dst else None
+
+
+def gather_sam_device(sam, dst=0):
+    """Gather each rank's SAM text held in a uint8 tensor (on the GPU with the nccl backend = RCCL over
+    xGMI, or on the CPU with gloo) to `dst`, concatenated in rank order = input order: one all-gather
+    of the lengths, then one all-gather of the texts padded to the longest (RCCL's gather is built
+    from point-to-point sends; a ring all-gather keeps every xGMI link busy).  Returns the merged
+    uint8 tensor on `dst`, None on the other ranks; the tensor itself without torch.distributed."""
+    import torch
+    import torch.distributed as td
+    if not (td.is_available() and td.is_initialized()) or td.get_world_size() == 1:
+        return sam
+    w = td.get_world_size()
+    n = torch.tensor([sam.numel()], dtype=torch.int64, device=sam.device)
+    lens = [torch.zeros_like(n) for _ in range(w)]
+    td.all_gather(lens, n)
+    lens = [int(x.item()) for x in lens]
+    top = max(lens)
+    buf = torch.zeros(top, dtype=torch.uint8, device=sam.device)
+    buf[:sam.numel()] = sam
+    parts = [torch.empty(top, dtype=torch.uint8, device=sam.device) for _ in range(w)]
+    td.all_gather(parts, buf)
+    if td.get_rank() != dst:
+        return None
+    return torch.cat([p[:l] for p, l in zip(parts, lens)])

@@ -76,6 +76,7 @@ EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_inde
            "gwa_sam_header", "gwa_index_close", "gwa_align_batch", "gwa_results_free", "gwa_free",
            "gwa_batch_create", "gwa_batch_create_pairs", "gwa_align_pairs", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
            "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_results_records", "gwa_batch_results_select", "gwa_batch_format",
+           "gwa_batch_sam_copy",
            "gwa_pipeline_open", "gwa_pipeline_align", "gwa_pipeline_align_file", "gwa_pipeline_stats",
            "gwa_pipeline_close", "gwa_reads_parse", "gwa_reads_free"]
 
@@ -115,6 +116,7 @@ def lib():
         L.gwa_batch_results_range.argtypes = [V, ctypes.c_uint32, ctypes.c_uint32, P(_Results)]
         L.gwa_batch_results_select.argtypes = [V, V, ctypes.c_uint32, P(_Results)]
         L.gwa_batch_format.argtypes = [V, P(U64)]
+        L.gwa_batch_sam_copy.argtypes = [V, V, P(U64)]
         L.gwa_reads_parse.argtypes = [ctypes.c_char_p, U64, I, I, P(_ReadBuf), P(U64)]
         L.gwa_reads_free.argtypes = [P(_ReadBuf)]
         L.gwa_pipeline_open.argtypes = [V, I, P(_Config), ctypes.c_uint32, I, P(V)]
@@ -528,6 +530,17 @@ class Batch:
         st = BatchStats()
         _check(lib().gwa_batch_stats(self.h, ctypes.byref(st)))
         return st
+
+    def sam_device(self):
+        """The SAM text of the last format_device() as a uint8 torch tensor on the batch's GPU (a
+        device-to-device copy; for dist.gather_sam_device over RCCL)."""
+        import torch
+        n = ctypes.c_uint64()
+        _check(lib().gwa_batch_sam_copy(self.h, None, ctypes.byref(n)))
+        t = torch.empty(n.value, dtype=torch.uint8, device="cuda")
+        if n.value:
+            _check(lib().gwa_batch_sam_copy(self.h, ctypes.c_void_p(t.data_ptr()), ctypes.byref(n)))
+        return t
 
     def results(self, first=0, count=None):
         res = _Results()

@@ -175,6 +175,12 @@ int gwa_batch_results(gwa_batch_t *b, gwa_results_t *out);
 /* The batch's SAM text written in HBM only (paired-end: pairing included); *sam_bytes = its size.
  * For timing the device side of the reporting path; gwa_batch_results copies the text out. */
 int gwa_batch_format(gwa_batch_t *b, uint64_t *sam_bytes);
+/* Device-to-device copy of the batch's SAM text as the last gwa_batch_format wrote it in HBM (input
+ * order, no header) into dst, device memory of the batch's GPU with room for *len bytes; with dst NULL
+ * only *len is set.  Fails unless the last formatting of the batch was gwa_batch_format.  For a
+ * device-side gather of the SAM of several GPUs over RCCL / xGMI (genome-weaver-align_amd/dist.py
+ * gather_sam_device; SURVEY.md §8e's optional collective). */
+int gwa_batch_sam_copy(gwa_batch_t *b, void *dst, uint64_t *len);
 /* SAM for reads [first, first+count) only (n_reads = count). */
 int gwa_batch_results_range(gwa_batch_t *b, uint32_t first, uint32_t count, gwa_results_t *out);
 void gwa_batch_free(gwa_batch_t *b);

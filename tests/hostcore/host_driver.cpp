@@ -33,7 +33,8 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
   // GWA_TEST_SLICE_SHIFT moves the first tier's DP slice off the diagonal (every edit then
   // overflows into the next tier): the slice fallback path gives the same SAM
   const int sl = 1 + (getenv("GWA_TEST_SLICE_SHIFT") ? atoi(getenv("GWA_TEST_SLICE_SHIFT")) : 0);
-  const Caps tiers[4] = {{256, kLdsHeap, 32, 32, 512, dpw, path, sl, 0}, {1024, 1024, 64, 64, 1024, dpw, path, 0, 0},
+  // (k >= 4, R >= 8: the GPU's hybrid heap holds as many entries as the arena, gwa_batch_run)
+  const Caps tiers[4] = {{256, R >= 8 ? 256 : kLdsHeap, 32, 32, 512, dpw, path, sl, 0}, {1024, 1024, 64, 64, 1024, dpw, path, 0, 0},
                          {4096, 4096, 256, 256, 4096, dpw, path, 0, 0}, {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 0}};
   // -m sf tiers (gwa_api.cpp kSfTiers)
   const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, sl, 32}, {2048, 2048, 64, 64, 2048, dpw, path, 0, 256},

@@ -61,12 +61,18 @@ def _rank_main(rank, world_size, port, outdir):
     dt = time.perf_counter() - t0 + 0.05 * rank  # ranks differ; the max must win
     mx = dist.max_over_ranks(dt)
     merged = dist.gather_sam(sam)
+    # the tensor form (the GPU path gathers device buffers over RCCL; gloo here, on the CPU)
+    import torch
+    dev_merged = dist.gather_sam_device(torch.frombuffer(bytearray(sam.encode()), dtype=torch.uint8))
     if rank == 0:
         with open(os.path.join(outdir, "merged.sam"), "w") as f:
             f.write(merged)
+        with open(os.path.join(outdir, "merged_tensor.sam"), "wb") as f:
+            f.write(dev_merged.numpy().tobytes())
         with open(os.path.join(outdir, "max.txt"), "w") as f:
             f.write("%r %r" % (mx, dt))
     else:
+        assert dev_merged is None
         with open(os.path.join(outdir, "rank1.txt"), "w") as f:
             f.write("%r %r" % (mx, dt))
     td.barrier()
@@ -82,6 +88,7 @@ def test_two_rank_shard_gather_equals_single(tmp_path):
     single = oi.align(reads, O.OrcConfig.default(k=2.0))
     merged = open(tmp_path / "merged.sam").read()
     assert merged == single
+    assert open(tmp_path / "merged_tensor.sam").read() == single
     m0, d0 = map(float, open(tmp_path / "max.txt").read().split())
     m1, d1 = map(float, open(tmp_path / "rank1.txt").read().split())
     assert m0 == m1 == max(d0, d1)

@@ -314,6 +314,23 @@ def test_pipeline_two_handles_in_memory(random_pair):
     assert st.device_kernel_s[0] > 0 and st.device_kernel_s[1] > 0
 
 
+def test_sam_device_copy_matches_results(random_pair):
+    # gwa_batch_sam_copy: the SAM text gwa_batch_format wrote in HBM, copied device to device into a
+    # torch buffer (the source of dist.gather_sam_device), equals the host results
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 1500, 100, 2, config_id=33)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
+    b = gwa.Batch(gi, gwa.AlignmentConfig(k=2.0), reads)
+    b.run()
+    n = b.format_device()
+    t = b.sam_device()
+    sam, _ = b.results()
+    b.close()
+    assert t.numel() == n and t.cpu().numpy().tobytes().decode() == sam == oi.align(reads, O.OrcConfig.default(k=2.0))
+
+
 def test_per_read_counters_match_oracle_stats(random_pair):
     # numFMIndexSearches, FMQuickScan steps and DP verifications per read, device vs the oracle's
     # instrumented restatement (the oracle defines the algorithmic counts)
