@@ -222,7 +222,7 @@ void launchFastqFields(const char *text, uint64_t len, const uint64_t *start, ui
 // one read's records, or (pairs mode, ps.np > 0) pair r's two mate lines
 __device__ __forceinline__ int samUnit(SamOut &o, const SamText &t, uint32_t r, const OutHeader *oh, const OutHit *hits,
                                        const uint16_t *cig, const PairSpec &ps) {
-  if (ps.np) return samPair(o, t, r, ps.np, oh, hits, cig, ps.minIns, ps.maxIns);
+  if (ps.np) return samPair(o, t, r, ps.np, oh, hits, cig, ps.minIns, ps.maxIns, ps.resc);
   return samRead(o, t, r, oh[r], hits, cig);
 }
 

@@ -137,6 +137,7 @@ struct gwa_batch {
   bool headerOnly = false;  // -m bd / -m bwa: the reference emits no SAM records (see gwa_batch_create)
   uint32_t pairs = 0;       // paired-end batch: mate 1 of pair i = read i, mate 2 = read pairs + i
   int32_t minIns = 0, maxIns = 0;
+  RescueOut *d_rescue = nullptr;  // paired-end: per pair, the mate-rescue result (pair_rescue_kernel)
   std::vector<std::pair<uint32_t, int>> deep;  // (read, tier) of every read rerun on a tier >= 1
 };
 
@@ -491,7 +492,7 @@ static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
                 b->d_stair, b->d_stairBase, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
-                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull};
+                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue};
   for (void *p : ps)
     if (p) (void)hipFree(p);
   // the text blobs (one allocation may back several of them)
@@ -825,6 +826,8 @@ struct Events {  // destroyed on every path out of gwa_batch_run
 };
 }  // namespace
 
+static SamText samText(const gwa_batch *b);
+
 int gwa_batch_run(gwa_batch_t *b) {
   try {
     gwa_index *ix = b->ix;
@@ -989,9 +992,38 @@ int gwa_batch_run(gwa_batch_t *b) {
       if (t + 1 < kNumTiers) ++t;
       else if (!refused) break;
     }
-    b->stats.search_ms = searchMs;
-    b->stats.kernel_ms = ems + qms + searchMs;
     if (n > 0) throw std::runtime_error(std::to_string(n) + " reads exceeded the largest search tier");
+    b->stats.search_ms = searchMs;
+    double rescueMs = 0;
+    if (b->pairs) {  // paired-end: mate rescue (orc_align_pairs rule 3), part of the alignment
+      Caps rc{};
+      rc.cigar = 512;
+      rc.dpWords = 2 * 4 * (kRescueWindow + 1);  // QW = 8: up to 4 blocks of 64 rows, full history
+      rc.path = 255 + kRescueWindow + 8;
+      rc.dpSlice = 0;
+      const uint64_t stride = laneBytesFor(4, rc);
+      uint32_t lanes = std::min<uint32_t>(b->pairs, 65536u);
+      lanes = (lanes + 63) / 64 * 64;
+      const size_t need = (size_t)(stride + ilvBytesFor(rc)) * lanes;
+      if (need > ix->scratchBytes) {
+        if (ix->scratch) HIPCHK(hipFree(ix->scratch));
+        ix->scratch = nullptr;
+        ix->scratchBytes = 0;
+        HIPCHK(hipMalloc(&ix->scratch, need));
+        ix->scratchBytes = need;
+      }
+      HIPCHK(hipEventRecord(e1, s));
+      launchPairRescue(lanes, ix->view, b->scfg, b->st, rv, samText(b), b->d_oh, b->d_hits, b->d_cig, b->pairs, b->minIns,
+                       b->maxIns, ix->scratch, stride, rc, b->d_rescue, s);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(e2, s));
+      HIPCHK(hipEventSynchronize(e2));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, e1, e2));
+      rescueMs = ms;
+    }
+    b->stats.rescue_ms = rescueMs;
+    b->stats.kernel_ms = ems + qms + searchMs + rescueMs;
     b->ran = true;
     return 0;
   } catch (std::exception &e) {
@@ -1090,7 +1122,7 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
   Events ev;
   HIPCHK(hipEventRecord(ev.e[0], s));
   const SamText t = samText(b);
-  const PairSpec ps{b->pairs, b->minIns, b->maxIns};
+  const PairSpec ps{b->pairs, b->minIns, b->maxIns, b->pairs ? b->d_rescue : nullptr};
   size_t tmpBytes = b->fmtTmpBytes;
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
                   b->d_fmtErr, nullptr, 0, s, ps);
@@ -1285,6 +1317,7 @@ int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_r
     (*out)->pairs = n;
     (*out)->minIns = min_insert;
     (*out)->maxIns = max_insert;
+    (*out)->d_rescue = devAlloc<RescueOut>(n);
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());

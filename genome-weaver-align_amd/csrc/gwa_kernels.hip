@@ -16,6 +16,7 @@
 
 #include "bsf_core.h"
 #include "sf_core.h"
+#include "sam_core.h"
 #include "kernels.h"
 
 namespace gwa {
@@ -264,6 +265,82 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
     }
     waveAppend(ovf, r, ovfList, ovfCount);
   }
+}
+
+// Paired-end mate rescue (orc_align_pairs rule 3, oracle/gwa_oracle.cpp peRescue; the build's own
+// design -- the reference has no paired-end path): for a pair without a proper pair whose mates are
+// one mapped and one without candidates, the unmapped mate is aligned by the search's own DP
+// (BsfLane::alignBlockDetailed, full history) inside the window the insert range allows next to the
+// anchor; a hit with at most max(k, m / 10) differences is written to out[i].  Persistent lanes over
+// the pairs, 64 per workgroup (the query words of each lane's mate in LDS).
+__global__ void __launch_bounds__(64) pair_rescue_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
+                                                         SamText t, const OutHeader *oh, const OutHit *hits,
+                                                         const uint16_t *cig, uint32_t np, int32_t minIns, int32_t maxIns,
+                                                         uint8_t *scratch, uint64_t laneStride, Caps caps, RescueOut *out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = gridDim.x * blockDim.x;
+  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
+  const LaneMem<4> L = laneMem<4>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+  __shared__ uint64_t qwLds[2 * 8 * 64];
+  for (uint32_t i = gid; i < np; i += total) {
+    int status = 0;
+    const PairChoice P = pairChoose(t, i, np, oh, hits, cig, minIns, maxIns);
+    if (P.ok && !P.a && ((P.fa != nullptr) != (P.fb != nullptr))) {
+      const OutHit &an = P.fa ? *P.fa : *P.fb;
+      const uint16_t *anc = P.fa ? P.ca : P.cb;
+      const uint32_t r = P.fa ? np + i : i;  // the mate without candidates
+      const int m = (int)reads.len[r];
+      BsfLane<4, 8> lane(ix, cfg, st, L, caps);
+      lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
+      lane.qwS = 64;
+      lane.initRead(reads.codes + reads.off[r], m);
+      const int countN = m > 0 && m <= 255 ? lane.buildMasks() : 0x7FFF;
+      const int k = lane.k;
+      if (m > 0 && m <= 255 && k >= 0 && countN <= k) {
+        const int kr = k > m / 10 ? k : m / 10;
+        const int64_t off = ix.contigOff[an.chr];
+        const int64_t clen = (an.chr + 1 < ix.nContig ? ix.contigOff[an.chr + 1] : (int64_t)ix.N) - off;
+        const int64_t s0 = off + (int64_t)an.pos - 1;
+        int64_t ws, we;
+        int strand;
+        if (an.strand == 0) {
+          strand = 1;
+          ws = s0 + minIns - m - kr;
+          we = s0 + maxIns + kr;
+        } else {
+          strand = 0;
+          const int64_t e0 = s0 + samRefLen(anc, an) - 1;
+          ws = e0 - maxIns + 1 - kr;
+          we = e0 - minIns + 1 + m + kr;
+        }
+        ws = ws > off ? ws : off;
+        we = we < off + clen ? we : off + clen;
+        if (we - ws >= m && we - ws <= kRescueWindow) {
+          int pos = 0, diff = 0, co = 0, cl = 0;
+          const int res = lane.alignBlockDetailed(strand, 0, m, ws, we, &pos, &diff, &co, &cl);
+          int32_t chr = 0, p = 0;
+          if (res == 0 && diff <= kr && cl <= kRescueCig && lane.translate(ws + pos + 1, &chr, &p) == 0) {
+            RescueOut &R = out[i];
+            R.hit.chr = chr; R.hit.pos = p; R.hit.matchLength = m; R.hit.qStart = 0; R.hit.qEnd = m;
+            R.hit.diff = diff; R.hit.strand = strand; R.hit.numHits = 1; R.hit.next = -1;
+            R.hit.cigarOff = 0; R.hit.cigarLen = (uint32_t)cl;
+            for (int j = 0; j < cl; ++j) R.cig[j] = lane.L.cigar()[co + j];
+            status = P.fa ? 2 : 1;
+          }
+        }
+      }
+    }
+    out[i].status = status;
+  }
+}
+
+void launchPairRescue(uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                      const ReadsView &reads, const SamText &t, const OutHeader *oh, const OutHit *hits,
+                      const uint16_t *cig, uint32_t np, int32_t minIns, int32_t maxIns, uint8_t *scratch,
+                      uint64_t laneStride, const Caps &caps, RescueOut *out, hipStream_t s) {
+  if (np == 0) return;
+  hipLaunchKernelGGL(pair_rescue_kernel, dim3((lanes + 63) / 64), dim3(64), 0, s, ix, cfg, st, reads, t, oh, hits, cig, np,
+                     minIns, maxIns, scratch, laneStride, caps, out);
 }
 
 // one thread per k-mer (IndexView::kmer)

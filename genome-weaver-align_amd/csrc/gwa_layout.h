@@ -173,6 +173,16 @@ GWA_HD uint32_t outReserve(uint32_t *ctr, uint32_t v) {
 #endif
 }
 
+// Paired-end mate rescue (orc_align_pairs rule 3, the build's own design): per pair, the rescued
+// mate's hit when the pair had no proper pair and only one mate had candidates
+constexpr int kRescueCig = 64;     // CIGAR ops of a rescued hit (at most 2 kr + 3 <= 53 for m <= 255)
+constexpr int kRescueWindow = 320; // longest rescue window (bases)
+struct RescueOut {
+  int32_t status;  // 0 none, 1 mate 1 rescued, 2 mate 2 rescued
+  OutHit hit;      // cigarOff 0 into cig
+  uint16_t cig[kRescueCig];
+};
+
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at
 // S/BidirectionalSuffixFilter.java:324-346)
 struct ScanRes {

@@ -37,7 +37,13 @@ size_t encodeScanTempBytes(uint32_t n);
 struct PairSpec {  // paired-end formatting: np pairs (mate 1 = read i, mate 2 = read np + i); np = 0: single-end
   uint32_t np;
   int32_t minIns, maxIns;
+  const RescueOut *resc;  // pair_rescue_kernel's output (or nullptr)
 };
+// paired-end mate rescue (orc_align_pairs rule 3) over np pairs, `lanes` persistent lanes
+void launchPairRescue(uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                      const ReadsView &reads, const SamText &t, const OutHeader *oh, const OutHit *hits,
+                      const uint16_t *cig, uint32_t np, int32_t minIns, int32_t maxIns, uint8_t *scratch,
+                      uint64_t laneStride, const Caps &caps, RescueOut *out, hipStream_t s);
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
                      uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
                      uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps);

@@ -432,17 +432,39 @@ GWA_HD void samMateLine(SamOut &o, const SamText &t, uint32_t r, const OutHit *h
   o.ch('\n');
 }
 
-// Pair i: choose the mates' hits (orc_align_pairs rules 1-3) and write both lines.  -1 where a
-// mate's search failed or the reference would throw.
-GWA_HD int samPair(SamOut &o, const SamText &t, uint32_t i, uint32_t np, const OutHeader *oh, const OutHit *hits,
-                   const uint16_t *cig, int32_t minIns, int32_t maxIns) {
-  const OutHeader &A = oh[i], &B = oh[np + i];
-  if ((A.status != ST_MAPPED && A.status != ST_UNMAPPED) || (B.status != ST_MAPPED && B.status != ST_UNMAPPED)) return -1;
-  const OutHit *ha = hits + A.hitOff, *hb = hits + B.hitOff;
-  const uint16_t *ca = cig + A.cigOff, *cb = cig + B.cigOff;
-  const int na = A.status == ST_MAPPED ? A.nChains : 0, nb = B.status == ST_MAPPED ? B.nChains : 0;
-  // candidates: the chain heads without a split and with a contig, in report order
+// The mates' candidates and the best proper pair of pair i (orc_align_pairs rules 1-2): fa / fb = each
+// mate's first candidate (a chain head without a split and with a contig, in report order), a / b =
+// the proper pair with the fewest differences (ties: the first in mate-1, then mate-2 order), or null.
+// ok = false where a mate's search failed.
+struct PairChoice {
   const OutHit *a = nullptr, *b = nullptr, *fa = nullptr, *fb = nullptr;
+  const uint16_t *ca = nullptr, *cb = nullptr;  // the CIGAR bases of mate 1's / mate 2's hits
+  bool ok = true;
+};
+
+// rule 2's test: one contig, opposite strands, forward start <= reverse end, template length in range
+GWA_HD bool pairProper(const SamText &t, const OutHit &u, const uint16_t *cu, const OutHit &v, const uint16_t *cv,
+                       int32_t minIns, int32_t maxIns) {
+  if (t.chrKey[u.chr] != t.chrKey[v.chr] || u.strand == v.strand) return false;
+  const OutHit &fw = u.strand == 0 ? u : v, &rv = u.strand == 0 ? v : u;
+  const uint16_t *rc = u.strand == 0 ? cv : cu;
+  const int64_t fs = fw.pos, re = (int64_t)rv.pos + samRefLen(rc, rv) - 1;
+  const int64_t tl = re - fs + 1;
+  return !(fs > re || tl < minIns || tl > maxIns);
+}
+
+GWA_HD PairChoice pairChoose(const SamText &t, uint32_t i, uint32_t np, const OutHeader *oh, const OutHit *hits,
+                             const uint16_t *cig, int32_t minIns, int32_t maxIns) {
+  PairChoice P;
+  const OutHeader &A = oh[i], &B = oh[np + i];
+  if ((A.status != ST_MAPPED && A.status != ST_UNMAPPED) || (B.status != ST_MAPPED && B.status != ST_UNMAPPED)) {
+    P.ok = false;
+    return P;
+  }
+  const OutHit *ha = hits + A.hitOff, *hb = hits + B.hitOff;
+  P.ca = cig + A.cigOff;
+  P.cb = cig + B.cigOff;
+  const int na = A.status == ST_MAPPED ? A.nChains : 0, nb = B.status == ST_MAPPED ? B.nChains : 0;
   int best = 0x7FFFFFFF;
   for (int x = 0, hx = 0; x < na; ++x) {
     const OutHit &u = ha[hx];
@@ -450,40 +472,50 @@ GWA_HD int samPair(SamOut &o, const SamText &t, uint32_t i, uint32_t np, const O
     while (ha[e].next >= 0) e = ha[e].next;
     const int next = e + 1;
     if (u.next < 0 && u.chr >= 0) {
-      if (!fa) fa = &u;
+      if (!P.fa) P.fa = &u;
       for (int y = 0, hy = 0; y < nb; ++y) {
         const OutHit &v = hb[hy];
         int f = hy;
         while (hb[f].next >= 0) f = hb[f].next;
         const int nextB = f + 1;
-        if (v.next < 0 && v.chr >= 0 && t.chrKey[u.chr] == t.chrKey[v.chr] && u.strand != v.strand) {
-          const OutHit &fw = u.strand == 0 ? u : v, &rv = u.strand == 0 ? v : u;
-          const uint16_t *rc = u.strand == 0 ? cb : ca;
-          const int64_t fs = fw.pos, re = (int64_t)rv.pos + samRefLen(rc, rv) - 1;
-          const int64_t tl = re - fs + 1;
-          if (!(fs > re || tl < minIns || tl > maxIns) && u.diff + v.diff < best) {
-            best = u.diff + v.diff;
-            a = &u;
-            b = &v;
-          }
+        if (v.next < 0 && v.chr >= 0 && u.diff + v.diff < best && pairProper(t, u, P.ca, v, P.cb, minIns, maxIns)) {
+          best = u.diff + v.diff;
+          P.a = &u;
+          P.b = &v;
         }
         hy = nextB;
       }
     }
     hx = next;
   }
-  if (!fb)
-    for (int y = 0, hy = 0; y < nb; ++y) {
-      const OutHit &v = hb[hy];
-      if (v.next < 0 && v.chr >= 0) { fb = &v; break; }
-      int f = hy;
-      while (hb[f].next >= 0) f = hb[f].next;
-      hy = f + 1;
-    }
-  const bool proper = a != nullptr;
+  for (int y = 0, hy = 0; y < nb && !P.fb; ++y) {
+    const OutHit &v = hb[hy];
+    if (v.next < 0 && v.chr >= 0) P.fb = &v;
+    int f = hy;
+    while (hb[f].next >= 0) f = hb[f].next;
+    hy = f + 1;
+  }
+  return P;
+}
+
+// Pair i: choose the mates' hits (orc_align_pairs rules 1-3; rule 3's rescued hit from `resc`, the
+// pair_rescue kernel's output) and write both lines.  -1 where a mate's search failed.
+GWA_HD int samPair(SamOut &o, const SamText &t, uint32_t i, uint32_t np, const OutHeader *oh, const OutHit *hits,
+                   const uint16_t *cig, int32_t minIns, int32_t maxIns, const RescueOut *resc) {
+  PairChoice P = pairChoose(t, i, np, oh, hits, cig, minIns, maxIns);
+  if (!P.ok) return -1;
+  const OutHit *a = P.a, *b = P.b;
+  const uint16_t *ca = P.ca, *cb = P.cb;
+  bool proper = a != nullptr;
   if (!proper) {
-    a = fa;
-    b = fb;
+    a = P.fa;
+    b = P.fb;
+    if (resc && resc[i].status != 0) {  // rule 3: the rescued mate is that mate's only candidate
+      const RescueOut &R = resc[i];
+      if (R.status == 1) { a = &R.hit; ca = R.cig; }
+      else { b = &R.hit; cb = R.cig; }
+      proper = a && b && pairProper(t, *a, ca, *b, cb, minIns, maxIns);
+    }
   }
   const bool sameChr = a && b && t.chrKey[a->chr] == t.chrKey[b->chr];
   int64_t tlen = 0;

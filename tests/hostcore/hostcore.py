@@ -12,7 +12,11 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        subprocess.check_call(["make", "-s", "-C", _HERE])
+        import fcntl
+        # one build at a time when several pytest-xdist workers start together
+        with open(os.path.join(_HERE, ".build.lock"), "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            subprocess.check_call(["make", "-s", "-C", _HERE])
         L = ctypes.CDLL(os.path.join(_HERE, "libgwa_hostcore.so"))
         L.hc_index_codes.restype = ctypes.c_void_p
         L.hc_index_codes.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]

@@ -491,6 +491,48 @@ def test_paired_end_insert_window_and_unmapped_mates(random_pair):
     assert got == oi.align_pairs(r1q, r2q, O.OrcConfig.default(k=2.0))
 
 
+def test_paired_end_mate_rescue_matches_oracle(random_pair):
+    """Rule 3 (mate rescue, pair_rescue_kernel): one mate carries 3-8 substitutions (or N runs),
+    beyond what -k 2 lets the search find; the DP inside the insert window beside the other mate
+    (window <= 320 bp, <= max(k, m/10) differences) rescues it.  Either mate may be the damaged one,
+    fragments sit at contig edges (clipped windows) and some are too damaged to rescue."""
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    rng = np.random.default_rng(57)
+    starts = np.concatenate([[0], np.cumsum(lengths)])
+    r1, r2 = [], []
+    for i in range(1500):
+        c = int(rng.integers(0, len(lengths)))
+        ins = int(rng.integers(260, 340))
+        if i % 50 == 0:
+            s = int(starts[c])  # fragment at the contig's left end
+        elif i % 50 == 1:
+            s = int(starts[c + 1]) - ins  # ... and at its right end
+        else:
+            s = int(starts[c] + rng.integers(0, lengths[c] - ins))
+        frag = codes[s:s + ins]
+        m1, m2 = frag[:100].copy(), synth.COMP[frag[ins - 100:][::-1]].copy()
+        if i % 3 == 1:
+            m1, m2 = m2, m1  # mate 1 on the reverse strand
+        bad = m2 if i % 4 else m1
+        nsub = int(rng.integers(3, 13)) if i % 11 else 0
+        for p in rng.choice(100, nsub, replace=False):
+            bad[p] = (bad[p] + int(rng.integers(1, 4))) % 4
+        if i % 13 == 0:
+            bad[40:43] = 4
+        q2 = None if i % 6 == 0 else "J" * 100
+        r1.append(("p%d/1" % i, synth.SYM[m1].tobytes().decode(), "I" * 100))
+        r2.append(("p%d/2" % i, synth.SYM[m2].tobytes().decode(), q2))
+    got = gwa.PairedEndAligner(gi, gwa.AlignmentConfig(k=2.0)).align_pairs(r1, r2)
+    exp = oi.align_pairs(r1, r2, O.OrcConfig.default(k=2.0))
+    if got != exp:
+        g, e = got.splitlines(), exp.splitlines()
+        bad = [(a, b) for a, b in zip(g, e) if a != b][:3]
+        raise AssertionError("SAM differs: %d vs %d lines; first diffs: %r" % (len(g), len(e), bad))
+    flags = [int(l.split("\t")[1]) for l in got.splitlines()]
+    assert sum(1 for f in flags if f & 0x2) > 2000  # most damaged mates are rescued into proper pairs
+
+
 def test_results_records_of_a_paired_batch(random_pair):
     # gwa_results_records on paired-end results: two mate lines per pair, each its own record (no
     # split linking: FLAG 0x41 / 0x81 are mates here, not a split record pair)
