@@ -1045,7 +1045,10 @@ struct BsfLane {
     uint64_t tp = 0;
     const int K = ix.kmerK;
     int i = 0;
-    while (i < m) {
+    // The scan stops at its (k+1)-th empty interval: the caller only reads numMismatches <= k and,
+    // under that condition, longestMatch (S/BidirectionalSuffixFilter.java:324-345), so a scan past
+    // k + 1 mismatches cannot change the result (the wrong strand of a read stops after ~3 restarts).
+    while (i < m && nmm <= k) {
       // at a restart from [0, N) (mark == i), the k-mer table answers the next K steps at once
       // when none of them is empty; otherwise the steps below run one by one
       if (K > 0 && i == mark && i + K <= m) {

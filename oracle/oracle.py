@@ -29,7 +29,8 @@ class OrcConfig(ctypes.Structure):
 
 class OrcStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
-        "fm_searches", "quick_steps", "rank_calls", "states", "max_heap", "hits", "sw", "max_hit_list")]
+        "fm_searches", "quick_steps", "rank_calls", "states", "max_heap", "hits", "sw", "max_hit_list",
+        "quick_steps_cut")]
 
 
 def build():
