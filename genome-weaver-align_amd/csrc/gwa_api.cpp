@@ -137,7 +137,8 @@ struct gwa_batch {
   bool headerOnly = false;  // -m bd / -m bwa: the reference emits no SAM records (see gwa_batch_create)
   uint32_t pairs = 0;       // paired-end batch: mate 1 of pair i = read i, mate 2 = read pairs + i
   int32_t minIns = 0, maxIns = 0;
-  RescueOut *d_rescue = nullptr;  // paired-end: per pair, the mate-rescue result (pair_rescue_kernel)
+  RescueOut *d_rescue = nullptr;  // paired-end: per pair, the pair choice and mate rescue (pair_rescue_kernel)
+  uint32_t *d_heavy = nullptr;     // paired-end: [pairs] heavy-pair list + its count (pair_choose_kernel)
   std::vector<std::pair<uint32_t, int>> deep;  // (read, tier) of every read rerun on a tier >= 1
 };
 
@@ -492,7 +493,7 @@ static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
                 b->d_stair, b->d_stairBase, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
-                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue};
+                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue, b->d_heavy};
   for (void *p : ps)
     if (p) (void)hipFree(p);
   // the text blobs (one allocation may back several of them)
@@ -1012,10 +1013,21 @@ int gwa_batch_run(gwa_batch_t *b) {
         HIPCHK(hipMalloc(&ix->scratch, need));
         ix->scratchBytes = need;
       }
+      uint32_t *heavyCount = b->d_heavy + b->pairs;
       HIPCHK(hipEventRecord(e1, s));
+      HIPCHK(hipMemsetAsync(heavyCount, 0, 4, s));
       launchPairRescue(lanes, ix->view, b->scfg, b->st, rv, samText(b), b->d_oh, b->d_hits, b->d_cig, b->pairs, b->minIns,
-                       b->maxIns, ix->scratch, stride, rc, b->d_rescue, s);
+                       b->maxIns, ix->scratch, stride, rc, b->d_rescue,
+                       getenv("GWA_PAIR_QUAD") ? atol(getenv("GWA_PAIR_QUAD")) : kPairQuad, b->d_heavy, heavyCount, s);
       HIPCHK(hipGetLastError());
+      uint32_t nHeavy = 0;
+      HIPCHK(hipMemcpyAsync(&nHeavy, heavyCount, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (nHeavy > b->pairs) throw std::runtime_error("pair choice: heavy-pair count out of range");
+      launchPairChoose(nHeavy, samText(b), b->d_oh, b->d_hits, b->d_cig, b->pairs, b->minIns, b->maxIns, b->d_heavy,
+                       getenv("GWA_PAIR_SORT_CAP") ? atoi(getenv("GWA_PAIR_SORT_CAP")) : kPairSortCap, b->d_rescue, s);
+      HIPCHK(hipGetLastError());
+      b->stats.heavy_pairs = nHeavy;
       HIPCHK(hipEventRecord(e2, s));
       HIPCHK(hipEventSynchronize(e2));
       float ms = 0;
@@ -1318,6 +1330,7 @@ int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_r
     (*out)->minIns = min_insert;
     (*out)->maxIns = max_insert;
     (*out)->d_rescue = devAlloc<RescueOut>(n);
+    (*out)->d_heavy = devAlloc<uint32_t>((size_t)n + 1);
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());

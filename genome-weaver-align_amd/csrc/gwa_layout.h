@@ -179,9 +179,17 @@ constexpr int kRescueCig = 64;     // CIGAR ops of a rescued hit (at most 2 kr +
 constexpr int kRescueWindow = 320; // longest rescue window (bases)
 struct RescueOut {
   int32_t status;  // 0 none, 1 mate 1 rescued, 2 mate 2 rescued
+  // the pair choice (rules 1-2), hit indices into the batch's hit pool, -1 = none: a / b = the proper
+  // pair with the fewest differences, fa / fb = each mate's first candidate
+  int32_t a, b, fa, fb;
   OutHit hit;      // cigarOff 0 into cig
   uint16_t cig[kRescueCig];
 };
+// pairs whose candidate counts multiply past kPairQuad are chosen by pair_choose_kernel (sorted
+// sweep, O(na log na + nb log nb)) instead of the all-pairs loop (tests lower both limits with
+// GWA_PAIR_QUAD / GWA_PAIR_SORT_CAP to drive every pair through the sweep or its fallback)
+constexpr int64_t kPairQuad = 64;
+constexpr int kPairSortCap = 4096;  // candidates of both mates one workgroup sorts in LDS
 
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at
 // S/BidirectionalSuffixFilter.java:324-346)

@@ -43,7 +43,12 @@ struct PairSpec {  // paired-end formatting: np pairs (mate 1 = read i, mate 2 =
 void launchPairRescue(uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                       const ReadsView &reads, const SamText &t, const OutHeader *oh, const OutHit *hits,
                       const uint16_t *cig, uint32_t np, int32_t minIns, int32_t maxIns, uint8_t *scratch,
-                      uint64_t laneStride, const Caps &caps, RescueOut *out, hipStream_t s);
+                      uint64_t laneStride, const Caps &caps, RescueOut *out, int64_t quad, uint32_t *heavy,
+                      uint32_t *heavyCount, hipStream_t s);
+// the pair choice of the heavy pairs pair_rescue_kernel listed (one workgroup each)
+void launchPairChoose(uint32_t nHeavy, const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig,
+                      uint32_t np, int32_t minIns, int32_t maxIns, const uint32_t *heavy, int sortCap, RescueOut *out,
+                      hipStream_t s);
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
                      uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
                      uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps);

@@ -453,6 +453,29 @@ GWA_HD bool pairProper(const SamText &t, const OutHit &u, const uint16_t *cu, co
   return !(fs > re || tl < minIns || tl > maxIns);
 }
 
+GWA_HD bool pairStatusOk(const OutHeader &A, const OutHeader &B) {
+  return (A.status == ST_MAPPED || A.status == ST_UNMAPPED) && (B.status == ST_MAPPED || B.status == ST_UNMAPPED);
+}
+// a mate's pairing candidates (chain heads without a split and with a contig): their count, and the
+// pool index of the first one in report order (-1 = none)
+GWA_HD int pairCandidates(const OutHeader &H, const OutHit *hits, int32_t *first) {
+  *first = -1;
+  const int nc = H.status == ST_MAPPED ? (int)H.nChains : 0;
+  const OutHit *h = hits + H.hitOff;
+  int count = 0;
+  for (int x = 0, hx = 0; x < nc; ++x) {
+    const OutHit &u = h[hx];
+    int e = hx;
+    while (h[e].next >= 0) e = h[e].next;
+    if (u.next < 0 && u.chr >= 0) {
+      if (*first < 0) *first = (int32_t)(H.hitOff + hx);
+      ++count;
+    }
+    hx = e + 1;
+  }
+  return count;
+}
+
 GWA_HD PairChoice pairChoose(const SamText &t, uint32_t i, uint32_t np, const OutHeader *oh, const OutHit *hits,
                              const uint16_t *cig, int32_t minIns, int32_t maxIns) {
   PairChoice P;
@@ -502,8 +525,20 @@ GWA_HD PairChoice pairChoose(const SamText &t, uint32_t i, uint32_t np, const Ou
 // pair_rescue kernel's output) and write both lines.  -1 where a mate's search failed.
 GWA_HD int samPair(SamOut &o, const SamText &t, uint32_t i, uint32_t np, const OutHeader *oh, const OutHit *hits,
                    const uint16_t *cig, int32_t minIns, int32_t maxIns, const RescueOut *resc) {
-  PairChoice P = pairChoose(t, i, np, oh, hits, cig, minIns, maxIns);
-  if (!P.ok) return -1;
+  PairChoice P;
+  if (resc) {  // the choice made by pair_rescue_kernel / pair_choose_kernel
+    if (!pairStatusOk(oh[i], oh[np + i])) return -1;
+    const RescueOut &R = resc[i];
+    P.a = R.a >= 0 ? hits + R.a : nullptr;
+    P.b = R.b >= 0 ? hits + R.b : nullptr;
+    P.fa = R.fa >= 0 ? hits + R.fa : nullptr;
+    P.fb = R.fb >= 0 ? hits + R.fb : nullptr;
+    P.ca = cig + oh[i].cigOff;
+    P.cb = cig + oh[np + i].cigOff;
+  } else {
+    P = pairChoose(t, i, np, oh, hits, cig, minIns, maxIns);
+    if (!P.ok) return -1;
+  }
   const OutHit *a = P.a, *b = P.b;
   const uint16_t *ca = P.ca, *cb = P.cb;
   bool proper = a != nullptr;

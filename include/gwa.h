@@ -116,7 +116,8 @@ typedef struct {
   uint64_t quick_text_runs; /* fm_quickscan text-mode runs (one 32-base 2-bit text window + N flags each) */
   double encode_ms;        /* read encoding on the device at the start of gwa_batch_run (part of kernel_ms) */
   double format_ms;        /* the last SAM formatting of the batch on the device (gwa_batch_format / results) */
-  double rescue_ms;        /* paired-end batches: the mate-rescue kernel (part of kernel_ms) */
+  double rescue_ms;        /* paired-end batches: pair choice + mate rescue kernels (part of kernel_ms) */
+  uint64_t heavy_pairs;    /* paired-end batches: pairs chosen by the sorted sweep (> 64 candidate combinations) */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);

@@ -535,6 +535,68 @@ def test_paired_end_mate_rescue_matches_oracle(random_pair):
     assert sum(1 for f in flags if f & 0x2) > 2000  # most damaged mates are rescued into proper pairs
 
 
+def _frag_pairs(codes, n, seed, subs, ins=(150, 300)):
+    """pairs from fragments anywhere in `codes` (both orientations), each mate with 0..subs substitutions"""
+    rng = np.random.default_rng(seed)
+    r1, r2 = [], []
+    for i in range(n):
+        L = int(rng.integers(ins[0], ins[1] + 1))
+        s = int(rng.integers(0, len(codes) - L))
+        frag = codes[s:s + L]
+        m1, m2 = frag[:100].copy(), synth.COMP[frag[L - 100:][::-1]].copy()
+        for m in (m1, m2):
+            for p in rng.choice(100, int(rng.integers(0, subs + 1)), replace=False):
+                m[p] = (m[p] + int(rng.integers(1, 4))) % 4
+        if i % 2:
+            m1, m2 = m2, m1
+        r1.append(("f%d/1" % i, synth.SYM[m1].tobytes().decode(), "I" * 100))
+        r2.append(("f%d/2" % i, synth.SYM[m2].tobytes().decode(), "J" * 100))
+    return r1, r2
+
+
+def _blobs(reads):
+    out = []
+    for f in range(3):
+        parts = [x[f].encode() for x in reads]
+        out += [b"".join(parts), np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)]
+    return tuple(out)
+
+
+@pytest.mark.parametrize("mode", ["sweep", "spread"])
+def test_paired_end_sorted_sweep_choice(random_pair, repetitive_pair, monkeypatch, mode):
+    """Rules 1-2 (fewest differences, ties by mate-1 then mate-2 report order) through
+    pair_choose_kernel: GWA_PAIR_QUAD=0 sends every pair whose mates both have candidates to the
+    LDS-sorted sliding-window sweep ("sweep"); GWA_PAIR_SORT_CAP=1 to its all-pairs loop spread over
+    the workgroup ("spread").  Genomes: random, repetitive, and the many-equal-hits one (200 copies of
+    a 300-base segment; -k 5 gives several candidates per mate), insert windows tight to unbounded."""
+    import gwa
+    import genomes
+    monkeypatch.setenv("GWA_PAIR_QUAD", "0")
+    if mode == "spread":
+        monkeypatch.setenv("GWA_PAIR_SORT_CAP", "1")
+    mh_codes, mh_names, mh_lengths, _ = genomes.many_hits()
+    mh_gi, mh_oi = _both(mh_codes, mh_names, mh_lengths)
+    rep_codes, rep_gi, rep_oi = repetitive_pair
+    codes, names, lengths, gi, oi = random_pair
+    cases = [(gi, oi, _frag_pairs(codes, 600, 63, 2), 2.0), (rep_gi, rep_oi, _frag_pairs(rep_codes, 600, 64, 2), 2.0),
+             (mh_gi, mh_oi, _frag_pairs(mh_codes, 600, 65, 3), 5.0)]
+    heavy = 0
+    for g, o, (r1, r2), k in cases:
+        for lo, hi in ((210, 390), (250, 260), (1, 1 << 20), (0, 200)):
+            got = gwa.PairedEndAligner(g, gwa.AlignmentConfig(k=k), lo, hi).align_pairs(r1, r2)
+            exp = o.align_pairs(r1, r2, O.OrcConfig.default(k=k), lo, hi)
+            if got != exp:
+                gl, el = got.splitlines(), exp.splitlines()
+                bad = [(x, y) for x, y in zip(gl, el) if x != y][:3]
+                raise AssertionError("k %g insert [%d, %d]: SAM differs: first diffs %r" % (k, lo, hi, bad))
+        b = gwa.Batch(g, gwa.AlignmentConfig(k=k), pair_blobs=(_blobs(r1), _blobs(r2)))
+        b.run()
+        heavy += b.stats().heavy_pairs
+        b.close()
+    assert heavy > 1000
+    mh_gi.close()
+
+
 def test_results_records_of_a_paired_batch(random_pair):
     # gwa_results_records on paired-end results: two mate lines per pair, each its own record (no
     # split linking: FLAG 0x41 / 0x81 are mates here, not a split record pair)
