@@ -20,7 +20,7 @@ import json
 import os
 import sys
 
-KERNELS = ["fm_quickscan_kernel", "bsf_search_kernel"]
+KERNELS = ["fm_quickscan_kernel", "bsf_search_kernel", "encodeLenKernel", "encodeWriteKernel", "samLenKernel", "samWriteKernel"]
 
 
 def _short(name):
