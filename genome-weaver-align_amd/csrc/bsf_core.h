@@ -755,6 +755,13 @@ struct BsfLane {
     if (nStates >= caps.arena) { status = ST_OVERFLOW; return -1; }
     return nStates++;
   }
+  // state word bit 26 (not a reference field): some state's nextSplit is, or was, this state -- it
+  // is a later member of a split chain (set by nextStateAfterSplit and update, never cleared)
+  static constexpr int32_t kStRef = 1 << 26;
+  GWA_HD void markRef(int s) {
+    S(s).state |= kStRef;
+    if (s == cacheIdx) cache.state |= kStRef;
+  }
   GWA_HD static int32_t packState(int ch, int mk, int pr, bool hm) {
     return ((ch & 7) << 5) | ((mk & 0xFF) << 8) | ((pr & 0xFF) << 16) | ((hm ? 1 : 0) << 24);
   }
@@ -818,6 +825,20 @@ struct BsfLane {
   // keys.  Entries are scanned 8 at a time with their loads issued together (deep tiers keep the
   // heap and the arena in HBM scratch; a refresh per report was a long dependent walk).
   GWA_HD void refreshKeysFor(int changed) {
+    if (!(S(changed).state & kStRef)) {
+      // no state holds `changed` as its nextSplit: the chains through it are its own queue entries
+      // (duplicates), found by index alone -- no arena reads, no chain walks
+      uint64_t key = 0;
+      int have = 0;
+      for (int i = 0; i < heapSize; ++i) {
+        const uint64_t e = hslot(i);
+        if ((int)(e & 0xFFFF) == changed) {
+          if (!have) { key = keyOf(changed); have = 1; }
+          hslot(i) = (key << 16) | (uint64_t)changed;
+        }
+      }
+      return;
+    }
     constexpr int U = 8;
     for (int i0 = 0; i0 < heapSize; i0 += U) {
       uint64_t e[U];
@@ -1152,21 +1173,29 @@ struct BsfLane {
     }
     return sc;
   }
-  // AlignmentResultHolder.add (:606-628)
+  // AlignmentResultHolder.add (:606-628).  The filter keeps the entries with totalDifferences <=
+  // minMismatches and totalMatchLength >= maxMatchLength; both thresholds only tighten and a listed
+  // chain never changes, so when neither moved since the last add, the entries that passed then
+  // (the first listOk) pass again and only the ones appended after it are tested: the same list,
+  // without a chain walk per entry per report (lists of equal hits in repeats reach thousands).
+  int listOk = 0;
   GWA_HD void resultAdd(int hit) {
     int newK = hitTotalDiff(hit);
     int matchLen = hitTotalMatch(hit);
     int newScore = hitTotalScore(hit);
+    const int mm0 = minMismatches, ml0 = maxMatchLength;
     if (newScore > bestScore) {
       if (matchLen > 0 && newK <= minMismatches) minMismatches = newK;
       bestScore = newScore;
     }
     if (maxMatchLength < matchLen) maxMatchLength = matchLen;
-    int n = 0;
-    for (int i = 0; i < listSize; ++i) {
+    const int keep = (minMismatches == mm0 && maxMatchLength == ml0) ? listOk : 0;
+    int n = keep;
+    for (int i = keep; i < listSize; ++i) {
       int e = L.list()[i];
       if (hitTotalDiff(e) <= minMismatches && hitTotalMatch(e) >= maxMatchLength) L.list()[n++] = e;
     }
+    listOk = n;
     if (n >= caps.list) { status = ST_OVERFLOW; listSize = n; return; }
     L.list()[n++] = hit;
     listSize = n;
@@ -1828,6 +1857,7 @@ struct BsfLane {
       for (int i = 0; i < R; ++i) t.nfa[i] = 0;
       t.state |= 1 << 25;  // updateClippedFlag
     }
+    t.state |= kStRef;  // a's nextSplit
     S(a) = d;
     S(b) = t;
     // keyOf(a) for the chain [a -> b] from the registers (chainScore with one split)
@@ -1848,6 +1878,7 @@ struct BsfLane {
       if (prev < 0) return -1;
     }
     S(prev).nextSplit = newS;
+    if (newS >= 0) markRef(newS);
     refreshKeysFor(prev);  // score() of every chain through prev changed
     return self;
   }
@@ -1966,7 +1997,7 @@ struct BsfLane {
       // the polled state and its split chain are read once into registers
       DState<R> C;
       loadState(base, C);
-      tr(1, (uint32_t)base, curWord(C), (uint32_t)C.state);
+      tr(1, (uint32_t)base, curWord(C), (uint32_t)(C.state & ~kStRef));
       // upperBoundOfScore of the polled chain (:380), taken before the walk (which only reads)
       const int ubScore = C.nextSplit < 0 ? stateScore(C, 0, true) : chainScore(base, true);
       int c = base;
@@ -2242,7 +2273,7 @@ struct BsfLane {
     maxMatchLength = 0;
     bestScore = -1;
     numFMIndexSearches = 0;
-    nStates = heapSize = nHits = listSize = nCigar = 0;
+    nStates = heapSize = nHits = listSize = nCigar = listOk = 0;
     cacheIdx = -1;
     xMode = 0;
     status = ST_UNMAPPED;
