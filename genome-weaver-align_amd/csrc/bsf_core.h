@@ -219,12 +219,12 @@ struct LaneMem {
   int lane, is;            // lane in the interleaved block, interleave stride (elements)
   // PriorityQueue array of (key << 16 | state index): entry i at heapP[i * hs].  In the slice
   // (hs = 1) or, for the first tier, in LDS interleaved across the workgroup (hs = 256).
-  // Hybrid heap (BsfLane::kHybridHeap, k >= 4 kernels): entries [0, heapH) in LDS at heapL[i * 256],
-  // the rest in the slice at heapG[i] (heapH = 0: all in the slice)
+  // Hybrid heap (HY kernels: k >= 4, and the sparse deep tiers): entries [0, heapH) in LDS at
+  // heapL[i * hsL], the rest in the slice at heapG[i] (heapH = 0: all in the slice)
   uint64_t *heapP;
   int hs;
   uint64_t *heapL = nullptr, *heapG = nullptr;
-  int heapH = 0;
+  int heapH = 0, hsL = 256;
   GWA_HD DState<R> *arena() const { return (DState<R> *)slice; }
   GWA_HD uint64_t *heap() const { return heapP; }
   GWA_HD int64_t *cand() const { return (int64_t *)(slice + oCand); }
@@ -816,7 +816,7 @@ struct BsfLane {
   // heap (HY; k >= 4 kernels: their heaps outgrow a small LDS array, deep heaps are rare), LDS for the
   // top slots and the slice beyond them -- one flat address either way
   GWA_HD uint64_t &hslot(int i) const {
-    if (HY) return i < L.heapH ? L.heapL[(size_t)i * 256] : L.heapG[i];
+    if (HY) return i < L.heapH ? L.heapL[(size_t)i * L.hsL] : L.heapG[i];
     return L.heap()[(size_t)i * L.hs];
   }
   // Re-key the queued entries whose split chain passes through state `changed` (its minK or its

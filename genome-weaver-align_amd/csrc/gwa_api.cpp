@@ -879,7 +879,9 @@ int gwa_batch_run(gwa_batch_t *b) {
       Caps caps;
       caps.sparse = 0;
       caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
-      if (t > 0 && !sf) {  // GWA_TIER_ARENA="a0,a1,a2,a3": arena / heap states of tiers >= 1 (tuning runs)
+      // GWA_TIER_ARENA="a0,a1,a2,a3": arena / heap states of tiers >= 1, and of tier 0 for the
+      // hybrid-heap (k >= 4) kernels, whose heap is not bounded by the LDS array (tuning runs)
+      if ((t > 0 || b->R >= 8) && !sf) {
         const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", t, (uint32_t)T.arena), 65536u);
         caps.arena = caps.heap = a;
         caps.hits = caps.list = (int)tierValue("GWA_TIER_HITS", t, (uint32_t)T.hits);  // hit list / report list
@@ -917,6 +919,9 @@ int gwa_batch_run(gwa_batch_t *b) {
           }
         }
       }
+      // a very sparse tier whose lanes fit one round of one workgroup per CU (256 CUs x 4 waves):
+      // its queue tops go to LDS (bsf_search_kernel LH 2; the 64 KiB array leaves one workgroup per CU)
+      const bool deepLds = !sf && t > 0 && caps.sparse >= 8 && lanes <= 65536u;
       const size_t need = (size_t)(stride + ilvBytesFor(caps)) * lanes;
       if (need > ix->scratchBytes) {
         if (ix->scratch) HIPCHK(hipFree(ix->scratch));
@@ -935,7 +940,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0 || hybrid, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (t == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                    ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
                    (uint32_t *)d_prof, -1);
       {
@@ -959,7 +964,7 @@ int gwa_batch_run(gwa_batch_t *b) {
                        (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s);
       else
-        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, t == 0 || hybrid, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (t == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                      ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1],
                      ovfCount, s);
 #endif

@@ -80,12 +80,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
   // first tier: the priority queue lives in LDS, entry i of thread t at heapLds[i * 256 + t]
   // (heap high-water marks are ~5 entries for k <= 2, 100 bp; larger heaps overflow to tier 1)
-  __shared__ uint64_t heapLds[LH ? kLdsHeap * 256 : 1];
-  if (LH) {
+  // LH 2: a sparse deep tier (caps.sparse >= 8, a few long searches, one workgroup per CU): each
+  // active lane holds the top kDeepLdsHeap * sparse / 256 entries of its queue in LDS, contiguous,
+  // and the rest in its slice -- the sift of a queue of thousands of states then waits on HBM for
+  // its lowest levels only
+  __shared__ uint64_t heapLds[LH == 2 ? kDeepLdsHeap : LH ? kLdsHeap * 256 : 1];
+  if (LH == 1) {
     L.heapP = heapLds + threadIdx.x;
     L.hs = 256;
     L.heapL = heapLds + threadIdx.x;  // hybrid heap (k >= 4): LDS for the top slots, the slice beyond
     L.heapH = kLdsHeap;
+  } else if (LH == 2) {
+    const int per = kDeepLdsHeap / 256 * caps.sparse;
+    L.heapL = heapLds + (threadIdx.x / caps.sparse) * per;
+    L.hsL = 1;
+    L.heapH = per;
   }
 #ifdef GWA_PROF
   // profiling build: `trace` is a [lanes][PR_N] cycle-counter array, slot PR_N-1 = wave lifetime
@@ -127,7 +136,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
     return;
   }
 #endif
-  typedef BsfLane<R, QW, (LH != 0 && R >= 8)> Lane;  // hybrid heap: k >= 4 kernels with the LDS heap
+  typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8))> Lane;  // hybrid heap: k >= 4 with the LDS heap, sparse tiers
   Lane lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
   if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
@@ -556,15 +565,15 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
                   hipStream_t s, uint32_t *trace, int traceRead) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
-  const int key = (R * 16 + QW) * 2 + (ldsHeap ? 1 : 0);
+  const int key = (R * 16 + QW) * 3 + (ldsHeap == 2 ? 2 : ldsHeap ? 1 : 0);
   switch (key) {
 #define GWA_CASE(RR, QQ, LL)                                                                                          \
-  case (RR * 16 + QQ) * 2 + LL:                                                                                       \
+  case (RR * 16 + QQ) * 3 + LL:                                                                                       \
     hipLaunchKernelGGL((bsf_search_kernel<RR, QQ, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
                        scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount,                          \
                        trace, traceRead);                                                                             \
     break;
-#define GWA_CASE2(RR, QQ) GWA_CASE(RR, QQ, 0) GWA_CASE(RR, QQ, 1)
+#define GWA_CASE2(RR, QQ) GWA_CASE(RR, QQ, 0) GWA_CASE(RR, QQ, 1) GWA_CASE(RR, QQ, 2)
     GWA_CASE2(4, 4)
     GWA_CASE2(4, 8)
     GWA_CASE2(8, 4)

@@ -105,6 +105,7 @@ struct StairTables {
 };
 constexpr int kStairLdsWords = 2048;  // 16 KiB of LDS per workgroup
 constexpr int kLdsHeap = 8;           // first-tier priority-queue capacity (entries, in LDS)
+constexpr int kDeepLdsHeap = 8192;    // LDS queue entries per workgroup of a sparse deep tier (64 KiB)
 
 // ---- per-read output ----
 enum : int32_t {

@@ -36,9 +36,20 @@ struct SamOut {
     if (p) p[n] = c;
     ++n;
   }
+  // Text copies run 16 bytes per pass with the 16 loads issued before any store: a record's name,
+  // sequence and quality (~250 B) then wait on memory ~16 times, not once per byte (the SAM writer is
+  // latency-bound: a few workgroups per CU, each lane formatting one record)
   GWA_HD void bytes(const char *s, uint64_t len) {
-    if (p)
-      for (uint64_t i = 0; i < len; ++i) p[n + i] = s[i];
+    if (p) {
+      for (uint64_t i = 0; i < len; i += 16) {
+        char b[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) b[k] = i + k < len ? s[i + k] : 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (i + k < len) p[n + i + k] = b[k];
+      }
+    }
     n += len;
   }
   template <unsigned long L>
@@ -46,16 +57,25 @@ struct SamOut {
     bytes(s, L - 1);
   }
   GWA_HD void num(int64_t v) {  // Integer.toString
-    char b[24];
-    int k = 0;
+    // the digits, least significant first, packed 8 per register (no runtime-indexed array, which
+    // would live in scratch memory on the device)
     const bool neg = v < 0;
     uint64_t u = neg ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    uint64_t d0 = 0, d1 = 0, d2 = 0;
+    int k = 0;
     do {
-      b[k++] = (char)('0' + (int)(u % 10));
-      u /= 10;
+      const uint64_t q = u / 10, dig = u - q * 10;
+      if (k < 8) d0 |= dig << (8 * k);
+      else if (k < 16) d1 |= dig << (8 * (k - 8));
+      else d2 |= dig << (8 * (k - 16));
+      ++k;
+      u = q;
     } while (u);
     if (neg) ch('-');
-    while (k) ch(b[--k]);
+    for (int i = k - 1; i >= 0; --i) {
+      const uint64_t w = i < 8 ? d0 : i < 16 ? d1 : d2;
+      ch((char)('0' + (int)((w >> (8 * (i & 7))) & 0xFF)));
+    }
   }
 };
 
@@ -65,6 +85,8 @@ GWA_HD bool qualAbsent(const SamText &t, uint32_t r) { return t.qual == nullptr 
 namespace samfmt {
 
 constexpr char kSym[5] = {'A', 'C', 'G', 'T', 'N'};
+// kSym[x] as a shift of one packed constant (a table lookup is a memory load per base on the device)
+GWA_HD char sym(unsigned x) { return (char)((0x4E54474341ULL >> (8 * x)) & 0xFF); }
 constexpr char kOp[8] = {'M', 'I', 'D', 'N', 'S', 'H', 'P', 'X'};
 
 GWA_HD char stateCh(int numHits) { return numHits > 0 ? (numHits == 1 ? 'U' : 'R') : 'N'; }
@@ -147,11 +169,19 @@ GWA_HD void chrName(SamOut &o, Ctx &cx, int chr) {
   } else cx.npe = true;  // null chr
 }
 
+// (16 positions per pass, loads first: SamOut::bytes)
 GWA_HD void emitSeq(SamOut &o, const Ctx &cx, int a, int b) {
   const uint8_t *c = cx.t.codes + cx.t.codeOff[cx.r];
-  for (int j = a; j < b; ++j) {
-    const uint8_t x = cx.strand == 0 ? c[j] : c[cx.m - 1 - j];
-    o.ch(kSym[cx.strand == 0 ? x : (x < 4 ? 3 - x : 4)]);
+  for (int j0 = a; j0 < b; j0 += 16) {
+    uint8_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int j = j0 + k;
+      x[k] = j < b ? (cx.strand == 0 ? c[j] : c[cx.m - 1 - j]) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (j0 + k < b) o.ch(sym(cx.strand == 0 ? x[k] : (x[k] < 4 ? 3 - x[k] : 4)));
   }
 }
 
@@ -161,7 +191,17 @@ GWA_HD void emitQual(SamOut &o, const Ctx &cx, int a, int b) {
     return;
   }
   const char *q = cx.t.qual + cx.q0;
-  for (int j = a; j < b; ++j) o.ch(cx.strand == 0 ? q[j] : q[cx.qn - 1 - j]);
+  for (int j0 = a; j0 < b; j0 += 16) {
+    char x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int j = j0 + k;
+      x[k] = j < b ? (cx.strand == 0 ? q[j] : q[cx.qn - 1 - j]) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (j0 + k < b) o.ch(x[k]);
+  }
 }
 
 GWA_HD void emitState(SamOut &o, const Ctx &cx, int head, int self) {
@@ -328,7 +368,15 @@ GWA_HD void samUnmapped(SamOut &o, const SamText &t, uint32_t r) {
   o.bytes(t.name + t.nameB[r], t.nameE[r] - t.nameB[r]);
   o.lit("\t68\t*\t0\t1\t\t*\t0\t0\t");
   const uint8_t *c = t.codes + t.codeOff[r];
-  for (uint32_t j = 0; j < t.codeLen[r]; ++j) o.ch(samfmt::kSym[c[j] > 4 ? 4 : c[j]]);
+  const uint32_t len = t.codeLen[r];
+  for (uint32_t j0 = 0; j0 < len; j0 += 16) {
+    uint8_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = j0 + k < len ? c[j0 + k] : 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (j0 + k < len) o.ch(samfmt::sym(x[k] > 4 ? 4 : x[k]));
+  }
   o.ch('\t');
   if (!qualAbsent(t, r)) o.bytes(t.qual + t.qualB[r], t.qualE[r] - t.qualB[r]);
   else o.ch('*');
@@ -412,7 +460,7 @@ GWA_HD void samMateLine(SamOut &o, const SamText &t, uint32_t r, const OutHit *h
   const int m = (int)t.codeLen[r];
   for (int j = 0; j < m; ++j) {
     const uint8_t x = rev ? c[m - 1 - j] : c[j];
-    o.ch(samfmt::kSym[!rev ? (x > 4 ? 4 : x) : (x < 4 ? 3 - x : 4)]);
+    o.ch(samfmt::sym(!rev ? (x > 4 ? 4 : x) : (x < 4 ? 3 - x : 4)));
   }
   o.ch('\t');
   if (qualAbsent(t, r)) {
