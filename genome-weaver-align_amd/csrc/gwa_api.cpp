@@ -528,9 +528,9 @@ static bool batchHead(gwa_index *ix, const gwa_config_t *cfg, uint32_t n, gwa_ba
   sc.k = cfg->k; sc.reportType = cfg->report_type; sc.topL = cfg->top_l; sc.numSplit = cfg->num_split;
   sc.matchScore = cfg->match; sc.mismatchPenalty = cfg->mismatch; sc.splitOpenPenalty = cfg->split_open;
   sc.indelEndSkip = cfg->indel_end_skip; sc.bandWidth = cfg->band_width;
-  // 14: run a wavefront's parked reports once they are 7/8 of its live lanes (16 and 14
-  // tie on i.i.d. text; 14 is 10 % faster on the repetitive hg19r genome)
-  sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 14;
+  // a wavefront runs its parked reports once they are waitQ16/16 of its live lanes; the default is
+  // set with the NFA size in batchTail (DESIGN.md §4 sweeps)
+  sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 0;
   sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
   sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
   sc.textCache = getenv("GWA_TEXT_CACHE") ? atoi(getenv("GWA_TEXT_CACHE")) : 0;
@@ -578,6 +578,9 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   }
   if (b->kmax > 31) throw std::runtime_error("k > 31 is not supported on the device path");
   b->R = b->kmax + 1 <= 4 ? 4 : b->kmax + 1 <= 8 ? 8 : b->kmax + 1 <= 16 ? 16 : 32;
+  // report-batch threshold: 14/16 for k <= 3 (C2: 14-16 tie, 12 is 2 % slower; hg19r favours 14),
+  // 10/16 for k >= 4 (C4 -m bsf: 8 / 10 / 12 / 14 / 16 -> 447 / 447 / 454 / 489 / 684 ms per 1M reads)
+  if (b->scfg.waitQ16 <= 0) b->scfg.waitQ16 = b->R >= 8 ? 10 : 14;
   std::vector<uint64_t> tab;
   std::vector<uint32_t> base;
   buildStairTables(lens, std::max(b->kmax, 0), tab, base);
