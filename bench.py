@@ -478,7 +478,23 @@ def main():
                        "disk via the page cache; index load and pipeline open excluded; reads_per_s is the second "
                        "pass over the file on the same pipeline, first_pass_* the first (it also pins the host "
                        "buffers); stage times summed over threads, second pass"}
-        log("end to end FASTQ -> SAM: %.0f reads/s (%d reads in %.2fs)" % (n_e2e / t_e2e, n_e2e, t_e2e))
+        # parity of the pipeline's output (outside all timing): the SAM file's records, byte for byte,
+        # equal the SAM text the timed batch wrote in HBM for the same reads
+        try:
+            with open(so, "rb") as f:
+                body = f.read()
+            h = 0
+            while h < len(body) and body[h:h + 1] == b"@":
+                h = body.index(b"\n", h) + 1
+            ref = batch.sam_device().cpu().numpy()
+            same = len(body) - h == ref.size and np.array_equal(np.frombuffer(body, dtype=np.uint8, offset=h), ref)
+            del body, ref
+        except Exception as ex:  # reported, never fatal to the line
+            same = False
+            e2e["parity_error"] = repr(ex)
+        e2e["identical_to_timed_batch"] = bool(same)
+        log("end to end FASTQ -> SAM: %.0f reads/s (%d reads in %.2fs), SAM %s the timed batch's"
+            % (n_e2e / t_e2e, n_e2e, t_e2e, "identical to" if same else "DIFFERS from"))
         for x in (fq, so):
             os.remove(x)
         os.rmdir(d)

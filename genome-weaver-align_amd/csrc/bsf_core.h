@@ -1012,8 +1012,10 @@ struct BsfLane {
     const int64_t last2 = (int64_t)((ix.N - 1) >> 5), lastN = (int64_t)((ix.N - 1) >> 6);
     const int64_t a = s >> 5, b = s >> 6;
     const int sa = (int)(s & 31) * 2, sn = (int)(s & 63);
-    const uint64_t a0 = ix.text2[a], a1 = a + 1 <= last2 ? ix.text2[a + 1] : 0ULL;
-    const uint64_t n0 = ix.textN[b], n1 = b + 1 <= lastN ? ix.textN[b + 1] : 0ULL;
+    // the second N word only when the 32 flags cross into it (sn > 32): its bits land above bit 31
+    // otherwise and the cast drops them
+    const uint64_t a0 = ix.text2[a], a1 = (sa != 0 && a + 1 <= last2) ? ix.text2[a + 1] : 0ULL;
+    const uint64_t n0 = ix.textN[b], n1 = (sn > 32 && b + 1 <= lastN) ? ix.textN[b + 1] : 0ULL;
     *codes = sa ? (a0 >> sa) | (a1 << (64 - sa)) : a0;
     *nb = (uint32_t)(sn ? (n0 >> sn) | (n1 << (64 - sn)) : n0);
   }
