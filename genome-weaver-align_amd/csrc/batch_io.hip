@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(64) samWriteKernel(SamText t, const OutHeader 
 
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
                      uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
-                     uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps) {
+                     uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps, uint64_t totalBytes) {
   const dim3 grid((n + 1 + 255) / 256);
   if (pass == 0) {
     hipLaunchKernelGGL(samLenKernel, grid, dim3(256), 0, s, t, oh, hits, cig, idx, first, n, len, err, ps);
@@ -298,11 +298,19 @@ void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, 
   } else {
     if (n == 0) return;
     const dim3 g64((n + 63) / 64);
-    // 24 KiB of staging (6 workgroups per CU) holds 64 single-end 100-150 bp records; pairs get 48 KiB
-    if (ps.np)
+    // Staging for 64 records: the smallest size that holds 64 records of the batch's average length
+    // with 3 % to spare (a workgroup whose records do not fit writes them directly, correct but
+    // uncoalesced), so more workgroups fit a CU: 20 KiB (8 per CU) for 100 bp, 24 KiB (6) for 150 bp
+    // single-end records; pairs 48 KiB
+    const uint64_t need = n ? totalBytes * 64 * 103 / 100 / n + 16 : 0;
+    if (ps.np || need > 32768)
       hipLaunchKernelGGL(samWriteKernel<49152>, g64, dim3(64), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
-    else
+    else if (need > 24576)
+      hipLaunchKernelGGL(samWriteKernel<32768>, g64, dim3(64), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
+    else if (need > 20480 || totalBytes == 0)
       hipLaunchKernelGGL(samWriteKernel<24576>, g64, dim3(64), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
+    else
+      hipLaunchKernelGGL(samWriteKernel<20480>, g64, dim3(64), 0, s, t, oh, hits, cig, idx, first, n, off, out, ps);
     FCHK(hipGetLastError());
   }
 }

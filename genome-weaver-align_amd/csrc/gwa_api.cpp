@@ -1175,7 +1175,7 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
   }
   growDev(&b->d_fmtText, &b->fmtTextCap, (size_t)total + 1);
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
-                  b->d_fmtErr, b->d_fmtText, 2, s, ps);
+                  b->d_fmtErr, b->d_fmtText, 2, s, ps, total);
   HIPCHK(hipEventRecord(ev.e[1], s));
   HIPCHK(hipEventSynchronize(ev.e[1]));
   float ms = 0;

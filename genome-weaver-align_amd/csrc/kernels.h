@@ -51,7 +51,7 @@ void launchPairChoose(uint32_t nHeavy, const SamText &t, const OutHeader *oh, co
                       hipStream_t s);
 void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, const uint16_t *cig, const uint32_t *idx,
                      uint32_t first, uint32_t n, uint64_t *len, uint64_t *off, void *scanTmp, size_t *scanTmpBytes,
-                     uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps);
+                     uint32_t *err, char *out, int pass, hipStream_t s, const PairSpec &ps, uint64_t totalBytes = 0);
 size_t samScanTempBytes(uint32_t n);
 void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipStream_t s);
 size_t laneBytesFor(int R, const Caps &c);  // per-lane slice
