@@ -28,6 +28,10 @@ METRIC = "reads/sec (whole node), 100 bp k≤2 vs hg19, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+# the one JSON line goes here (main points fd 1 at stderr for everything else)
+JSON_OUT = sys.stdout
+
+
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
@@ -317,6 +321,13 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args)
+    # stdout carries exactly one JSON line (rank 0): whatever else writes to fd 1 in this process or
+    # its children -- torch / gloo / RCCL C++ logging such as "[Gloo] Rank 0 is connected to 1 peer
+    # ranks" -- is sent to stderr
+    global JSON_OUT
+    sys.stdout.flush()
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
@@ -614,7 +625,7 @@ def main():
                    "sam_gather": gather},
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=JSON_OUT, flush=True)
     if hg is None:
         batch.close()
     if dist:
@@ -742,7 +753,7 @@ def bench_c5(args, gi, codes, names, lengths, gname, rank, world, dist, dev, t_i
                       "tier_reads": list(st.tier_reads), "tier_ms": [round(x, 3) for x in st.tier_ms],
                       "cpu_baseline_1thread": cpu1, "parity": parity, "index_build_s": t_index}}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=JSON_OUT, flush=True)
     batch.close()
     if dist:
         tdist.destroy_process_group()
