@@ -415,24 +415,33 @@ def main():
     # HBM on every rank, gathered in rank order (= input order) over RCCL / xGMI
     gather = None
     if dist and torch.cuda.device_count() >= world:
+        # every rank first agrees that its text is ready (a rank that fails to copy it would leave the
+        # others blocked inside the collective)
         try:
+            mine_t = batch.sam_device()
+            ok = 1.0
+        except Exception as e:
+            mine_t, ok, gather = None, 0.0, {"error": repr(e)}
+        flag = torch.tensor([ok])
+        tdist.all_reduce(flag, op=tdist.ReduceOp.MIN)
+        if float(flag[0]) < 1.0:
+            gather = gather or {"error": "another rank could not copy its SAM text"}
+        else:
             torch.cuda.synchronize()
             barrier()
             t0 = time.perf_counter()
-            merged = gdist.gather_sam_device(batch.sam_device())
+            merged = gdist.gather_sam_device(mine_t)
             torch.cuda.synchronize()
             tg = time.perf_counter() - t0
             tot = gdist.all_gather_floats(float(sam_bytes))
             gather = {"seconds": tg, "bytes_per_rank": tot, "backend": "nccl (RCCL)",
                       "merged_bytes": int(merged.numel()) if merged is not None else None,
                       "GBps_gathered": sum(tot) / tg / 1e9 if tg > 0 else None,
-                      "note": "all-gather of the lengths, then of the texts padded to the longest; rank 0 keeps "
-                              "the concatenation in rank order"}
+                      "note": "all-gather of the lengths, then each rank's text sent once, point to point, into "
+                              "its slice of rank 0's merged buffer (rank order = input order)"}
             if merged is not None and int(merged.numel()) != int(sum(tot)):
                 gather["error"] = "merged size differs from the sum of the ranks' SAM sizes"
-            del merged
-        except Exception as e:  # reported, never fatal to the timing
-            gather = {"error": repr(e)}
+            del merged, mine_t
     elif dist:
         gather = {"skipped": "ranks share a GPU (RCCL needs one GPU per rank)"}
 

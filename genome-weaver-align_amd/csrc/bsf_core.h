@@ -217,7 +217,7 @@ struct LaneMem {
   uint32_t oHeap, oCand, oHits, oList, oCigar;  // byte offsets in the slice
   uint32_t oPath;          // byte offset of the path plane in the chunk
   int lane, is;            // lane in the interleaved block, interleave stride (elements)
-  // PriorityQueue array of (key << 16 | state index): entry i at heapP[i * hs].  In the slice
+  // PriorityQueue array of (key << KS | state index): entry i at heapP[i * hs].  In the slice
   // (hs = 1) or, for the first tier, in LDS interleaved across the workgroup (hs = 256).
   // Hybrid heap (HY kernels: k >= 4, and the sparse deep tiers): entries [0, heapH) in LDS at
   // heapL[i * hsL], the rest in the slice at heapG[i] (heapH = 0: all in the slice)
@@ -356,9 +356,12 @@ struct Overflow {};  // thrown only on host test builds; device uses status code
 
 // QW = 2-bit query words per strand held in registers (4: reads <= 128 bp, 8: <= 255 bp); the
 // DP then needs at most DB = QW / 2 blocks of 64 rows.  HY: hybrid heap (hslot).
-template <int R, int QW = 8, bool HY = false>
+// KS: bits of the state index in a queue entry (key << KS | index): 16 on the BSF path (its 48-bit
+// key; arenas <= 65536 states), 24 on the SF path (40-bit key; arenas up to 2^24 states).
+template <int R, int QW = 8, bool HY = false, int KS = 16>
 struct BsfLane {
   static constexpr int DB = QW / 2;
+  static constexpr uint64_t IDXM = (1ULL << KS) - 1ULL;
   const IndexView &ix;
   const SearchConfig &cfg;
   const StairTables &st;
@@ -373,6 +376,11 @@ struct BsfLane {
   int numFMIndexSearches;
   int nStates, heapSize, nHits, listSize, nCigar;
   int status;  // ST_*
+  int ovfWhat = 0;  // OV_* bits: which per-lane capacity a ST_OVERFLOW exceeded (the host grows it)
+  GWA_HD void ovf(int what) {
+    status = ST_OVERFLOW;
+    ovfWhat |= what;
+  }
   // instrumentation
   int quickSteps, blocks, saReads, maxHeap, kmerLookups, shortSteps, textSteps, textRuns;
   int numSW, verifyBytes;  // DP verifications and their §8d bytes (instrumentation)
@@ -752,13 +760,14 @@ struct BsfLane {
   }
 
   GWA_HD int allocState() {
-    if (nStates >= caps.arena) { status = ST_OVERFLOW; return -1; }
+    if (nStates >= caps.arena) { ovf(OV_ARENA); return -1; }
     return nStates++;
   }
   // state word bit 26 (not a reference field): some state's nextSplit is, or was, this state -- it
   // is a later member of a split chain (set by nextStateAfterSplit and update, never cleared)
   static constexpr int32_t kStRef = 1 << 26;
   GWA_HD void markRef(int s) {
+    if (s == cacheIdx) flushCache();  // a referenced state is never a deferred one
     S(s).state |= kStRef;
     if (s == cacheIdx) cache.state |= kStRef;
   }
@@ -832,9 +841,9 @@ struct BsfLane {
       int have = 0;
       for (int i = 0; i < heapSize; ++i) {
         const uint64_t e = hslot(i);
-        if ((int)(e & 0xFFFF) == changed) {
+        if ((int)(e & IDXM) == changed) {
           if (!have) { key = keyOf(changed); have = 1; }
-          hslot(i) = (key << 16) | (uint64_t)changed;
+          hslot(i) = (key << KS) | (uint64_t)changed;
         }
       }
       return;
@@ -847,26 +856,26 @@ struct BsfLane {
       for (int u = 0; u < U; ++u) e[u] = i0 + u < heapSize ? hslot(i0 + u) : 0ULL;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int idx = (int)(e[u] & 0xFFFF);
+        const int idx = (int)(e[u] & IDXM);
         nx[u] = (i0 + u < heapSize && idx != changed) ? S(idx).nextSplit : -1;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (i0 + u >= heapSize) continue;
-        const int idx = (int)(e[u] & 0xFFFF);
+        const int idx = (int)(e[u] & IDXM);
         int hit = idx == changed ? 1 : 0, t = nx[u];
         while (hit == 0 && t >= 0) {  // (single-exit loop: see quickScan)
           hit = t == changed ? 1 : 0;
           t = hit ? t : S(t).nextSplit;
         }
-        if (hit) hslot(i0 + u) = (keyOf(idx) << 16) | (uint64_t)idx;
+        if (hit) hslot(i0 + u) = (keyOf(idx) << KS) | (uint64_t)idx;
       }
     }
   }
   GWA_HD void refreshKeys() {
     for (int i = 0; i < heapSize; ++i) {
-      const int idx = (int)(hslot(i) & 0xFFFF);
-      hslot(i) = (keyOf(idx) << 16) | (uint64_t)idx;
+      const int idx = (int)(hslot(i) & IDXM);
+      hslot(i) = (keyOf(idx) << KS) | (uint64_t)idx;
     }
   }
   // java.util.PriorityQueue.offer / poll on cached keys.  The element moves are exactly Java's
@@ -874,12 +883,12 @@ struct BsfLane {
   // 8 levels) at once, poll reads children and grandchildren together, so a heap operation waits
   // on memory once per 8 (offer) or 2 (poll) levels instead of once per level.
   GWA_HD void queueAddKeyed(uint64_t e) {
-    if (heapSize >= caps.heap) { status = ST_OVERFLOW; return; }
+    if (heapSize >= caps.heap) { ovf(OV_HEAP); return; }
 #ifdef GWA_HEAP_STATS
     maxHeap = heapSize + 1 > maxHeap ? heapSize + 1 : maxHeap;
 #endif
     const int kk = heapSize++;
-    const uint64_t ek = e >> 16;
+    const uint64_t ek = e >> KS;
     constexpr int MAXD = 8;
     uint64_t av[MAXD];
     int ai[MAXD];
@@ -899,7 +908,7 @@ struct BsfLane {
     const int depth = 31 - __builtin_clz((unsigned)kk + 1u);
     int t = MAXD;
 #pragma unroll
-    for (int d = MAXD - 1; d >= 0; --d) t = (d >= depth || ek >= (av[d] >> 16)) ? d : t;
+    for (int d = MAXD - 1; d >= 0; --d) t = (d >= depth || ek >= (av[d] >> KS)) ? d : t;
 #pragma unroll
     for (int d = 0; d < MAXD; ++d)
       if (d < t) hslot(d == 0 ? kk : ai[d - 1]) = av[d];
@@ -908,13 +917,13 @@ struct BsfLane {
       while (pos > 0) {
         const int parent = (pos - 1) >> 1;
         const uint64_t p = hslot(parent);
-        if (ek >= (p >> 16)) break;
+        if (ek >= (p >> KS)) break;
         hslot(pos) = p;
         pos = parent;
       }
     }
     hslot(pos) = e;
-    tr(9, (uint32_t)(e & 0xFFFF), (uint32_t)kk, (uint32_t)pos);
+    tr(9, (uint32_t)(e & IDXM), (uint32_t)kk, (uint32_t)pos);
   }
   GWA_HD int queuePoll() {
     if (heapSize == 0) return -1;
@@ -924,7 +933,7 @@ struct BsfLane {
     if (s != 0) {
       const int n = heapSize, half = n >> 1, capm1 = caps.heap - 1;
       int kk = 0;
-      const uint64_t xk = x >> 16;
+      const uint64_t xk = x >> KS;
       int go = kk < half;  // single-exit loop (no break): see quickScan
       while (go) {
         // children c0,c1 and grandchildren g0..g3 of kk (indices clamped into the array; entries
@@ -935,9 +944,9 @@ struct BsfLane {
         const uint64_t g0 = hslot(g <= capm1 ? g : capm1), g1 = hslot(g + 1 <= capm1 ? g + 1 : capm1);
         const uint64_t g2 = hslot(g + 2 <= capm1 ? g + 2 : capm1), g3 = hslot(g + 3 <= capm1 ? g + 3 : capm1);
         // level 1
-        const int right = (c + 1 < n && (c0 >> 16) > (c1 >> 16)) ? 1 : 0;
+        const int right = (c + 1 < n && (c0 >> KS) > (c1 >> KS)) ? 1 : 0;
         const uint64_t cv = right ? c1 : c0;
-        if (xk <= (cv >> 16)) {
+        if (xk <= (cv >> KS)) {
           go = 0;
         } else {
           hslot(kk) = cv;
@@ -948,9 +957,9 @@ struct BsfLane {
         if (go) {
           const int c2 = (kk << 1) + 1;
           const uint64_t d0 = right ? g2 : g0, d1 = right ? g3 : g1;
-          const int right2 = (c2 + 1 < n && (d0 >> 16) > (d1 >> 16)) ? 1 : 0;
+          const int right2 = (c2 + 1 < n && (d0 >> KS) > (d1 >> KS)) ? 1 : 0;
           const uint64_t dv = right2 ? d1 : d0;
-          if (xk <= (dv >> 16)) {
+          if (xk <= (dv >> KS)) {
             go = 0;
           } else {
             hslot(kk) = dv;
@@ -961,12 +970,12 @@ struct BsfLane {
       }
       hslot(kk) = x;
     }
-    tr(10, (uint32_t)(result & 0xFFFF), (uint32_t)heapSize, (uint32_t)(x & 0xFFFF));
-    return (int)(result & 0xFFFF);
+    tr(10, (uint32_t)(result & IDXM), (uint32_t)heapSize, (uint32_t)(x & IDXM));
+    return (int)(result & IDXM);
   }
   GWA_HD void queueAdd(int e) {
     if (e < 0) return;
-    queueAddKeyed((keyOf(e) << 16) | (uint64_t)e);
+    queueAddKeyed((keyOf(e) << KS) | (uint64_t)e);
   }
 
   // ---- FMQuickScan.scanMismatchLocations (S/FMQuickScan.java:66-94) ----
@@ -1145,14 +1154,14 @@ struct BsfLane {
 
   // ---- hits (R/ReadHit.java) ----
   GWA_HD int newHit(int32_t chr, int32_t pos, int ml, int qs, int qe, int diff, int strand, int cigOff, int cigLen, int numHits) {
-    if (nHits >= caps.hits) { status = ST_OVERFLOW; return -1; }
+    if (nHits >= caps.hits) { ovf(OV_HITS); return -1; }
     DHit &h = L.hits()[nHits];
     h.chr = chr; h.pos = pos; h.matchLength = ml; h.qStart = qs; h.qEnd = qe; h.diff = diff; h.strand = strand;
     h.numHits = numHits; h.next = -1; h.cigarOff = cigOff; h.cigarLen = cigLen; h.pad = 0;
     return nHits++;
   }
   GWA_HD int putCigarOp(int type, int len) {
-    if (nCigar >= caps.cigar) { status = ST_OVERFLOW; return -1; }
+    if (nCigar >= caps.cigar) { ovf(OV_CIGAR); return -1; }
     L.cigar()[nCigar++] = (uint16_t)((len << 3) | type);
     return 0;
   }
@@ -1198,7 +1207,7 @@ struct BsfLane {
       if (hitTotalDiff(e) <= minMismatches && hitTotalMatch(e) >= maxMatchLength) L.list()[n++] = e;
     }
     listOk = n;
-    if (n >= caps.list) { status = ST_OVERFLOW; listSize = n; return; }
+    if (n >= caps.list) { ovf(OV_LIST); listSize = n; return; }
     L.list()[n++] = hit;
     listSize = n;
   }
@@ -1209,7 +1218,7 @@ struct BsfLane {
     int arr[8];
     int n = 0;
     for (int t = head; t >= 0; t = L.hits()[t].next) {
-      if (n >= 8) { status = ST_OVERFLOW; return head; }
+      if (n >= 8) { ovf(OV_CHAIN); return head; }
       arr[n++] = t;
     }
     const int headStrand = L.hits()[head].strand;
@@ -1321,7 +1330,7 @@ struct BsfLane {
     const int N = (int)(refEnd - refStart);
     ++numSW;
     verifyBytes += (2 * N + 7) / 8 + (N + 7) / 8 + 32 * bMax;
-    if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords) { status = ST_OVERFLOW; return -1; }
+    if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords) { ovf(OV_DP); return -1; }
     uint64_t pA[DB], pC[DB], pG[DB], pT[DB];
 #pragma unroll
     for (int r = 0; r < DB; ++r) {
@@ -1350,7 +1359,7 @@ struct BsfLane {
     int bestTail = 0, bestDiff = 0;
     // the window: N <= m + 2k + 2 <= 32 QW + 64 bases
     RefWindow<QW + 2, QW / 2 + 1> rw;
-    if (N > 32 * (QW + 2)) { status = ST_OVERFLOW; return -1; }
+    if (N > 32 * (QW + 2)) { ovf(OV_DP); return -1; }
     rw.load(ix.text2, ix.textN, ix.N, refStart);
     GWA_PT(tdf);
     // Column c of the history holds, per block, what the reference's zero-initialised arrays hold
@@ -1511,7 +1520,7 @@ struct BsfLane {
         int bp, bn;
         if (slice) {
           const int rr = row - (col + 1 - c0 - 17);
-          if (rr < 0 || rr >= 32) { status = ST_OVERFLOW; return -1; }  // off the slice: next tier
+          if (rr < 0 || rr >= 32) { ovf(OV_SLICE); return -1; }  // off the slice: next tier
           const uint64_t h = h8[(size_t)(col + 1) * is];
           bp = (int)(h >> rr) & 1;
           bn = (int)(h >> (32 + rr)) & 1;
@@ -1533,14 +1542,14 @@ struct BsfLane {
         break;
       }
     }
-    if (bad) { status = ST_OVERFLOW; return -1; }
+    if (bad) { ovf(OV_CIGAR); return -1; }
     GWA_PA(PR_DPT, tdt);
     const int off = nCigar;
     if (!seenM) {
       diff -= adj;  // the whole path is the leading clip (left = plen, right = 0)
       if (right > 0 && putCigarOp(4, right) < 0) return -1;
     } else {
-      if (nCigar + 2 * nRuns + 4 > cap) { status = ST_OVERFLOW; return -1; }
+      if (nCigar + 2 * nRuns + 4 > cap) { ovf(OV_CIGAR); return -1; }
       cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
       diff -= adj + pendAdj;
       if (pendL > 0 && putCigarOp(4, pendL) < 0) return -1;
@@ -1896,6 +1905,7 @@ struct BsfLane {
     oh->searchShort = 0;
     oh->numSW = oh->verifyBytes = 0;
     oh->poolFail = 0;
+    oh->ovfWhat = 0;
     oh->nChains = oh->nHits = oh->nCigar = 0;
     oh->status = ST_UNMAPPED;
     {
@@ -1996,6 +2006,7 @@ struct BsfLane {
       if (numFMIndexSearches > upperSearches) return SS_DONE;
       GWA_PT(tp);
       const int base = queuePoll();
+      if (base != cacheIdx) flushCache();  // the deferred state stays queued
       // the polled state and its split chain are read once into registers
       DState<R> C;
       loadState(base, C);
@@ -2011,14 +2022,17 @@ struct BsfLane {
       }
       GWA_PA(PR_POLL, tp);
       if ((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) {
+        flushCache();  // verify reads the chain from the arena
         pendingBase = base;
         return SS_REPORT;
       }
-      if ((C.state & 0x1F) == 0x1F) return SS_CONTINUE;  // isFinished
+      // the checks below drop the polled state (a deferred one is chain-free: dead from here)
       const int nm = (int)(((uint32_t)C.state >> 8) & 0xFF);
-      if (nm > minMismatches) return SS_CONTINUE;
-      if (minMismatches - nm < 0) return SS_CONTINUE;
-      if (ubScore < 0 || ubScore < bestScore) return SS_CONTINUE;
+      if ((C.state & 0x1F) == 0x1F || nm > minMismatches || minMismatches - nm < 0 || ubScore < 0 ||
+          ubScore < bestScore) {  // isFinished / pruned
+        dropIfCached(base);
+        return SS_CONTINUE;
+      }
       xBase = base;
       xC = c;
       xCS = C;
@@ -2046,7 +2060,7 @@ struct BsfLane {
       if (ch >= 0) {
         storeStateWord(xC, xCS.state);
         GWA_PT(tn);
-        int ns = nextStateLocal(xC, xCS, ch);
+        int ns = nextStateLocal(xC, xCS, ch, first && xC == xBase && deferrable(xCS));
         GWA_PA(PR_LOOP, tn);
         if (ns == -2) return SS_DONE;
         if (ns >= 0) {
@@ -2084,19 +2098,33 @@ struct BsfLane {
           const int ns = nextStateAfterSplit(xCS, clip != 0, &key);
           if (ns == -2) return SS_DONE;
           if (ns >= 0) {
-            if (xC == xBase) queueAddKeyed((key << 16) | (uint64_t)ns);  // update(base, base, ns) == ns
+            if (xC == xBase) queueAddKeyed((key << KS) | (uint64_t)ns);  // update(base, base, ns) == ns
             else queueAdd(update(xBase, xC, ns));
           }
         }
       }
     }
+    if (xC == xBase && deferrable(xCS)) dropIfCached(xC);  // the expanded chain-free state is done
     GWA_PA(PR_SPLIT, ts);
     return SS_CONTINUE;
   }
 
   // ---- register cache of the most recently created state (the usual next poll) ----
-  int cacheIdx = -1;
+  // Write-back deferral: a new state that no split chain holds (nextSplit < 0, no kStRef) stays
+  // only in the cache (cacheDirty) until it is evicted.  The usual next poll returns it, and when
+  // its own next base is accepted the reference drops it (:386-396: the child is pushed, the parent
+  // is not) -- its arena copy would never be read, so it is never written.  Every other path writes
+  // it back first (flushCache): a poll of another state, a report, a chain operation, an eviction
+  // by a state other than its accepted first child.
+  int cacheIdx = -1, cacheDirty = 0;
   DState<R> cache;
+  GWA_HD void flushCache() {
+    if (cacheDirty) {
+      L.arena()[cacheIdx] = cache;
+      cacheDirty = 0;
+    }
+  }
+  GWA_HD static bool deferrable(const DState<R> &d) { return d.nextSplit < 0 && !(d.state & kStRef); }
   GWA_HD void loadState(int idx, DState<R> &d) {
 #ifdef GWA_NO_CACHE
     d = L.arena()[idx];
@@ -2106,10 +2134,17 @@ struct BsfLane {
 #endif
   }
   GWA_HD void storeStateWord(int idx, int32_t w) {
-    L.arena()[idx].state = w;
+    if (!(idx == cacheIdx && cacheDirty)) L.arena()[idx].state = w;
     if (idx == cacheIdx) cache.state = w;
   }
-  GWA_HD void invalidateCache() { cacheIdx = -1; }
+  GWA_HD void invalidateCache() {
+    flushCache();
+    cacheIdx = -1;
+  }
+  // the polled state `base` (the cache, chain-free) is dead: the reference drops it here
+  GWA_HD void dropIfCached(int base) {
+    if (base == cacheIdx && cacheDirty) cacheDirty = 0;
+  }
   GWA_HD int qcode(int strand, int i) const { return (int)((qword(strand, i >> 5) >> (2 * (i & 31))) & 3); }
   // one chain member's term of score()/upperBoundOfScore() with ns splits after it
   GWA_HD int stateScore(const DState<R> &d, int ns, bool upper) const {
@@ -2161,18 +2196,24 @@ struct BsfLane {
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
     return true;
   }
-  // the child in a new arena slot (stays cached); -1 null, -2 overflow
-  GWA_HD int nextStateLocal(int c, const DState<R> &cs, int ch) {
+  // the child in a new arena slot (stays cached); -1 null, -2 overflow.  parentDead: c is the
+  // polled chain-free state and this child is its accepted next base (the reference drops c), so a
+  // deferred c is not written back
+  GWA_HD int nextStateLocal(int c, const DState<R> &cs, int ch, bool parentDead) {
     DState<R> d;
     if (!buildChild(cs, ch, d)) return -1;
     int id = allocState();
     if (id < 0) return -2;
-    L.arena()[id] = d;
 #ifndef GWA_NO_CACHE
+    if (parentDead && c == cacheIdx) cacheDirty = 0;
+    flushCache();
     cache = d;
     cacheIdx = id;
+    if (deferrable(d)) cacheDirty = 1;
+    else L.arena()[id] = d;
+#else
+    L.arena()[id] = d;
 #endif
-    (void)c;
     return id;
   }
 
@@ -2188,7 +2229,7 @@ struct BsfLane {
   // intermediate states, which nothing references (chain-free, not queued, not reported).  The run
   // stops before any state that the loop would treat otherwise -- report, prune, empty or rejected
   // first child, non-text interval -- and that state is pushed as the reference pushes it.
-  GWA_HD uint64_t heapKeyAt(int i) const { return hslot(i) >> 16; }
+  GWA_HD uint64_t heapKeyAt(int i) const { return hslot(i) >> KS; }
   GWA_HD bool heapNoop(uint64_t *bound) const {
     const int kk = heapSize;
     *bound = ~0ULL;
@@ -2259,10 +2300,14 @@ struct BsfLane {
       moved = 1;
     }
     if (!moved) return ns;
+    // ns (the run's first state, deferred or written) is never referenced: the run's last state
+    // takes its place in the queue
     const int id = allocState();
     if (id < 0) return -2;
-    L.arena()[id] = cache;
+    cacheDirty = 0;
     cacheIdx = id;
+    if (deferrable(cache)) cacheDirty = 1;
+    else L.arena()[id] = cache;
     return id;
   }
 
@@ -2277,8 +2322,10 @@ struct BsfLane {
     numFMIndexSearches = 0;
     nStates = heapSize = nHits = listSize = nCigar = listOk = 0;
     cacheIdx = -1;
+    cacheDirty = 0;
     xMode = 0;
     status = ST_UNMAPPED;
+    ovfWhat = 0;
     stairBad = 0;
     stairInLds = 0;
     stairTab = nullptr;
@@ -2306,6 +2353,7 @@ struct BsfLane {
     oh->nHits = 0;
     oh->nCigar = 0;
     oh->poolFail = 0;
+    oh->ovfWhat = ovfWhat;
     if (status == ST_OVERFLOW || status == ST_ERROR) { oh->status = status; return; }
     bool hasHitF = minMismatches <= k && listSize > 0;
     if (!hasHitF) { oh->status = ST_UNMAPPED; return; }

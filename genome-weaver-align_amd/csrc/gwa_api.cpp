@@ -876,21 +876,40 @@ int gwa_batch_run(gwa_batch_t *b) {
     int cur = 0;
     uint32_t n = nSearch;
     const int m = std::max(b->maxM, 1);
-    int t = 0, regrow = 0;
+    int t = 0, regrow = 0, launches = 0;
+    // Reads that overflow the last tier rerun on it with the exceeded capacities doubled (OV_* bits
+    // the kernel ORs into d_count[15]), as often as needed: no read the reference would finish is
+    // refused for capacity.  The hard limits are the state index of a queue entry (BsfLane KS: 2^16
+    // states on the BSF path, 2^24 on the SF path) and the scratch budget; past them the batch fails
+    // with the read count and the limit.  (BSF arenas are bounded by the search itself: <= 20m + 5
+    // FM steps each create <= 1 state and, with num_split = 1, <= 2 split states per state expanded,
+    // ~15.4k states for m = 255, well under 2^16.)
+    int gArena = 0, gHits = 0, gList = 0, gCigar = 0, gCand = 0;
+    const int arenaMaxLog = sf ? 24 : 16;
     while (n > 0) {
-      const Tier &T = sf ? kSfTiers[t] : kTiers[t];
+      if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
+      const int tb = std::min(t, kNumTiers - 1);  // t > kNumTiers - 1: the last tier, grown
+      const Tier &T = sf ? kSfTiers[tb] : kTiers[tb];
       Caps caps;
       caps.sparse = 0;
       caps.arena = T.arena; caps.heap = T.heap; caps.hits = T.hits; caps.list = T.list; caps.cigar = T.cigar;
       // GWA_TIER_ARENA="a0,a1,a2,a3": arena / heap states of tiers >= 1, and of tier 0 for the
       // hybrid-heap (k >= 4) kernels, whose heap is not bounded by the LDS array (tuning runs)
-      if ((t > 0 || b->R >= 8) && !sf) {
-        const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", t, (uint32_t)T.arena), 65536u);
+      if ((tb > 0 || b->R >= 8) && !sf) {
+        const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", tb, (uint32_t)T.arena), 65536u);
         caps.arena = caps.heap = a;
-        caps.hits = caps.list = (int)tierValue("GWA_TIER_HITS", t, (uint32_t)T.hits);  // hit list / report list
-        caps.cigar = (int)tierValue("GWA_TIER_CIGAR", t, (uint32_t)T.cigar);
+        caps.hits = caps.list = (int)tierValue("GWA_TIER_HITS", tb, (uint32_t)T.hits);  // hit list / report list
+        caps.cigar = (int)tierValue("GWA_TIER_CIGAR", tb, (uint32_t)T.cigar);
       }
       caps.cand = T.cand;
+      if (tb == kNumTiers - 1) {  // the grown last tier
+        caps.arena <<= gArena;
+        caps.heap <<= gArena;
+        caps.hits <<= gHits;
+        caps.list <<= gList;
+        caps.cigar <<= gCigar;
+        caps.cand <<= gCand;
+      }
       // k >= 4 (R >= 8): a hybrid heap, its top slots in LDS and the rest in the slice, holding as
       // many entries as the arena has states (k >= 4 heaps outgrow the 8-slot LDS heap of tier 0)
       const bool hybrid = !sf && b->R >= 8;
@@ -899,33 +918,35 @@ int gwa_batch_run(gwa_batch_t *b) {
       const int nref = m + 2 * b->kmax + 2;
       caps.dpWords = 2 * bMax * (nref + 1);
       caps.path = m + nref + 8;
-      caps.dpSlice = t == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
+      caps.dpSlice = tb == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
       const uint64_t stride = laneBytesFor(b->R, caps);
-      uint32_t lanes = std::min<uint32_t>(n, tierValue("GWA_TIER_LANES", t, T.maxLanes));
+      const uint64_t per = stride + ilvBytesFor(caps);
+      const uint64_t budget = scratchBudget(ix);
+      if (per * 256 > budget)
+        throw std::runtime_error(std::to_string(n) + " reads need more than " + std::to_string(budget >> 20) +
+                                 " MiB of search scratch per 256 lanes (" + std::to_string(caps.arena) +
+                                 " states per lane): the device memory budget is exhausted");
+      uint32_t lanes = std::min<uint32_t>(n, tierValue("GWA_TIER_LANES", tb, T.maxLanes));
       lanes = (lanes + 255) / 256 * 256;
-      {  // deep tiers: as many lanes as the scratch budget allows (at least one workgroup)
-        const uint64_t per = stride + ilvBytesFor(caps);
-        const uint64_t cap = std::max<uint64_t>(256, scratchBudget(ix) / per / 256 * 256);
-        lanes = (uint32_t)std::min<uint64_t>(lanes, cap);
-      }
-      if (t > 0 && !sf) {
+      // deep tiers: as many lanes as the scratch budget allows (at least one workgroup)
+      lanes = (uint32_t)std::min<uint64_t>(lanes, std::max<uint64_t>(256, budget / per / 256 * 256));
+      if (tb > 0) {
         // a deep tier with few reads: 64 / s reads per wavefront (every s-th lane), the largest s
         // whose n x s lanes stay within GWA_SPARSE_LANES (default 262144) and the scratch budget
-        const uint64_t per = stride + ilvBytesFor(caps), maxSparse = tierValue("GWA_SPARSE_LANES", 0, 262144u);
-        const uint64_t budget = scratchBudget(ix);
-        for (uint32_t s = 64; s >= 2; s /= 2) {
-          const uint64_t sl = ((uint64_t)n * s + 255) / 256 * 256;
-          if (sl <= maxSparse && sl * per <= budget) {
+        const uint64_t maxSparse = tierValue("GWA_SPARSE_LANES", 0, 262144u);
+        for (uint32_t sp = 64; sp >= 2; sp /= 2) {
+          const uint64_t sl = ((uint64_t)n * sp + 255) / 256 * 256;
+          if (sl <= maxSparse && sl * per <= budget && (!sf || tb == kNumTiers - 1)) {
             lanes = (uint32_t)sl;
-            caps.sparse = (int32_t)s;
+            caps.sparse = (int32_t)sp;
             break;
           }
         }
       }
       // a very sparse tier whose lanes fit one round of one workgroup per CU (256 CUs x 4 waves):
       // its queue tops go to LDS (bsf_search_kernel LH 2; the 64 KiB array leaves one workgroup per CU)
-      const bool deepLds = !sf && t > 0 && caps.sparse >= 8 && lanes <= 65536u;
-      const size_t need = (size_t)(stride + ilvBytesFor(caps)) * lanes;
+      const bool deepLds = !sf && tb > 0 && caps.sparse >= 8 && lanes <= 65536u;
+      const size_t need = (size_t)per * lanes;
       if (need > ix->scratchBytes) {
         if (ix->scratch) HIPCHK(hipFree(ix->scratch));
         ix->scratch = nullptr;
@@ -933,9 +954,11 @@ int gwa_batch_run(gwa_batch_t *b) {
         HIPCHK(hipMalloc(&ix->scratch, need));
         ix->scratchBytes = need;
       }
-      uint32_t *ovfCount = b->d_count + 1 + t;
+      uint32_t *ovfCount = b->d_count + 1 + tb;
+      uint32_t *ovfBits = b->d_count + 15;
       HIPCHK(hipMemsetAsync(ovfCount, 0, 4, s));
-      HIPCHK(hipMemsetAsync(b->d_count + 8 + t, 0, 4, s));
+      HIPCHK(hipMemsetAsync(b->d_count + 8 + tb, 0, 4, s));
+      HIPCHK(hipMemsetAsync(ovfBits, 0, 4, s));
       HIPCHK(hipEventRecord(e1, s));
       const OutSlots os = outSlots(b);
 #ifdef GWA_PROF
@@ -943,9 +966,9 @@ int gwa_batch_run(gwa_batch_t *b) {
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (t == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
-                   ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s,
-                   (uint32_t *)d_prof, -1);
+      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+                   ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount,
+                   ovfBits, s, (uint32_t *)d_prof, -1);
       {
         std::vector<uint64_t> pv((size_t)lanes * PR_N);
         HIPCHK(hipMemcpyAsync(pv.data(), d_prof, pv.size() * 8, hipMemcpyDeviceToHost, s));
@@ -965,11 +988,11 @@ int gwa_batch_run(gwa_batch_t *b) {
       if (sf)
         launchSfSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv,
                        (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh, os,
-                       ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1], ovfCount, s);
+                       ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s);
       else
-        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (t == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
-                     ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + t, b->d_list[cur ^ 1],
-                     ovfCount, s);
+        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+                     ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1],
+                     ovfCount, ovfBits, s);
 #endif
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(e2, s));
@@ -979,29 +1002,50 @@ int gwa_batch_run(gwa_batch_t *b) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, e1, e2));
       searchMs += ms;
-      b->stats.tier_reads[t] += n;
-      b->stats.tier_ms[t] += ms;
-      n = ctr[1 + t];
+      b->stats.tier_reads[tb] += n;
+      b->stats.tier_ms[tb] += ms;
+      if (getenv("GWA_VERBOSE"))
+        fprintf(stderr, "[gwa] tier %d: %u reads on %u lanes (sparse %d; arena %d hits %d list %d cigar %d cand %d): %.1f ms, %u overflow (bits 0x%x)\n",
+                t, n, lanes, caps.sparse, caps.arena, caps.hits, caps.list, caps.cigar, caps.cand, ms, ctr[1 + tb], ctr[15]);
+      n = ctr[1 + tb];
+      const uint32_t bits = ctr[15];
       cur ^= 1;
       if (n > 0) {  // the reads rerun on the next tier (instrumentation, gwa_batch_read_counters)
         std::vector<uint32_t> ids(n);
         HIPCHK(hipMemcpyAsync(ids.data(), b->d_list[cur], n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        const int nt = std::min(t + 1, kNumTiers - 1);
-        for (uint32_t r : ids) b->deep.push_back({r, nt});
+        for (uint32_t r : ids) b->deep.push_back({r, t + 1});
       }
       b->poolUsedH = std::min<uint64_t>(ctr[12], b->poolHits);
       b->poolUsedC = std::min<uint64_t>(ctr[13], b->poolCig);
       const bool refused = ctr[14] > 0;
       if (refused) {  // reads whose reported hits did not fit the pool: grow it, rerun them
-        if (++regrow > 8) break;
+        if (++regrow > 8) throw std::runtime_error("output pool growth did not converge");
         growPool(b, ctr[12], ctr[13], s);
         HIPCHK(hipMemsetAsync(b->d_count + 14, 0, 4, s));
       }
-      if (t + 1 < kNumTiers) ++t;
-      else if (!refused) break;
+      if (n > 0 && t >= kNumTiers - 1) {  // overflow of the last tier: grow what was exceeded
+        if (bits & (OV_CHAIN | OV_DP))
+          throw std::runtime_error(std::to_string(n) + (bits & OV_CHAIN ? " reads with a split chain of more than 8 pieces"
+                                                                        : " reads with a DP window beyond the read-length limit"));
+        if (bits & (OV_ARENA | OV_HEAP)) {
+          int lg = 0;
+          while ((1 << lg) < caps.arena) ++lg;
+          if (lg >= arenaMaxLog)
+            throw std::runtime_error(std::to_string(n) + " reads need more than 2^" + std::to_string(arenaMaxLog) +
+                                     " search states (the queue-entry state index)");
+          ++gArena;
+        }
+        if (bits & OV_HITS) ++gHits;
+        if (bits & OV_LIST) ++gList;
+        if (bits & OV_CIGAR) ++gCigar;
+        if (bits & OV_CAND) ++gCand;
+        if (!(bits & (OV_ARENA | OV_HEAP | OV_HITS | OV_LIST | OV_CIGAR | OV_CAND)) && !refused)
+          throw std::runtime_error(std::to_string(n) + " reads exceeded the largest search tier (overflow bits " +
+                                   std::to_string(bits) + ")");
+      }
+      ++t;
     }
-    if (n > 0) throw std::runtime_error(std::to_string(n) + " reads exceeded the largest search tier");
     b->stats.search_ms = searchMs;
     double rescueMs = 0;
     if (b->pairs) {  // paired-end: mate rescue (orc_align_pairs rule 3), part of the alignment

@@ -71,8 +71,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
                                                          const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                                                          uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
                                                          const int32_t *chrRank,
-                                                         uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *trace,
-                                                         int traceRead) {
+                                                         uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
+                                                         uint32_t *ovfBits, uint32_t *trace, int traceRead) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
   // scratch = [lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]
@@ -130,6 +130,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
         lane.writeSearchOutput(oh + r, os, r);
         if (lane.trace) trace[0] = (uint32_t)lane.traceN;
         ovf = oh[r].status == ST_OVERFLOW;
+        if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
       }
       waveAppend(ovf, r, ovfList, ovfCount);
     }
@@ -206,6 +207,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
       lane.writeSearchOutput(oh + r, os, r);
       if (lane.trace) trace[0] = (uint32_t)lane.traceN;
       ovf = oh[r].status == ST_OVERFLOW;
+      if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
       phase = IDLE;
     }
     waveAppend(ovf, r, ovfList, ovfCount);
@@ -222,7 +224,7 @@ template <int R, int QW>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES)))
 sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
                  uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
-                 const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount) {
+                 const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
   uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
@@ -243,6 +245,9 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
     lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
     lane.pmS = 256;
   }
+  // the grown last tier (few reads, long searches): every caps.sparse-th lane only, so the searches
+  // run on separate wavefronts instead of serialising inside one (bsf_search_kernel's sparse tiers)
+  if (caps.sparse > 1 && ((gid & 63) % (uint32_t)caps.sparse) != 0) return;
   for (;;) {
     const uint64_t act = __ballot(1);
     const int lid = __lane_id();
@@ -264,6 +269,7 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
       lane.initRead(reads.codes + reads.off[r], m);
       lane.sfSearch();
       lane.writeSearchOutput(h, os, r);
+      h->states = lane.created;  // (nStates is the arena's high-water mark: slots are recycled)
       h->quickSteps = lane.quickSteps;
       h->blocks = 0;  // (all Occ blocks are in searchBlocks on this path)
       h->kmerLookups = lane.kmerLookups;
@@ -271,6 +277,7 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
       h->quickSa = 0;
       h->quickText = 0;
       ovf = h->status == ST_OVERFLOW;
+      if (ovf) atomicOr(ovfBits, (uint32_t)h->ovfWhat);
     }
     waveAppend(ovf, r, ovfList, ovfCount);
   }
@@ -561,7 +568,7 @@ void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,
                   const StairTables &st, const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n,
                   uint8_t *scratch, uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,
-                  const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
+                  const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
                   hipStream_t s, uint32_t *trace, int traceRead) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
@@ -570,7 +577,7 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
 #define GWA_CASE(RR, QQ, LL)                                                                                          \
   case (RR * 16 + QQ) * 3 + LL:                                                                                       \
     hipLaunchKernelGGL((bsf_search_kernel<RR, QQ, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
-                       scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount,                          \
+                       scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits,                 \
                        trace, traceRead);                                                                             \
     break;
 #define GWA_CASE2(RR, QQ) GWA_CASE(RR, QQ, 0) GWA_CASE(RR, QQ, 1) GWA_CASE(RR, QQ, 2)
@@ -591,14 +598,15 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
 void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                     const Caps &caps, OutHeader *oh, const OutSlots &os,
-                    const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, hipStream_t s) {
+                    const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
+                    hipStream_t s) {
   if (n == 0) return;
   dim3 grid((lanes + 255) / 256);
   switch (R * 16 + QW) {
 #define GWA_SF(RR, QQ)                                                                                               \
   case RR * 16 + QQ:                                                                                                 \
     hipLaunchKernelGGL((sf_search_kernel<RR, QQ>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,      \
-                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount);                                  \
+                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);                         \
     break;
     GWA_SF(4, 4)
     GWA_SF(4, 8)

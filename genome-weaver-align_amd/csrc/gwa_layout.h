@@ -116,6 +116,14 @@ enum : int32_t {
   ST_TOO_LONG = 4,  // read longer than the device path supports
 };
 
+// OutHeader.ovfWhat: the per-lane capacities a ST_OVERFLOW read exceeded (Caps fields)
+enum : int32_t {
+  OV_ARENA = 1, OV_HEAP = 2, OV_HITS = 4, OV_CIGAR = 8, OV_LIST = 16, OV_CAND = 32,
+  OV_CHAIN = 64,   // a split chain of more than 8 pieces (sortSplits)
+  OV_DP = 128,     // a DP window / history larger than the lane's (fixed by the read length)
+  OV_SLICE = 256,  // a traceback left the first tier's DP slice (any later tier keeps whole columns)
+};
+
 // chr codes in OutHit.chr
 enum : int32_t { CHR_NULL = -1, CHR_EMPTY = -2, CHR_STAR = -3 };
 
@@ -148,6 +156,7 @@ struct OutHeader {
   // search FM steps answered by one text character (M_TEXT)
   int32_t verifyBytes;  // SURVEY.md §8d verify bytes: ceil(2n/8) + ceil(n/8) of each n-base window + 32 B Peq per block
   int32_t quickText;    // text-mode runs of the quick scan (each reads one 32-base text window: textWin)
+  int32_t ovfWhat;      // ST_OVERFLOW: OV_* bits of the capacities exceeded
 };
 
 // Where reads write their reported hits: read r owns the fixed slot hits[r * hitCap, + hitCap) and

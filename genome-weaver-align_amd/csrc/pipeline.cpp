@@ -121,6 +121,28 @@ class BufPool {
       freePageable_.pop_back();
     }
   }
+  // free pinned buffers of at least `cap` bytes
+  uint64_t countPinned(size_t cap) {
+    std::lock_guard<std::mutex> g(mu);
+    uint64_t n = 0;
+    for (auto *b : free_) n += b->cap >= cap ? 1 : 0;
+    return n;
+  }
+  // unpin the free pinned buffers smaller than `cap` (they can never serve a request of that size);
+  // returns how many and their bytes
+  void releasePinnedBelow(size_t cap, uint64_t *n, uint64_t *bytes) {
+    std::lock_guard<std::mutex> g(mu);
+    *n = *bytes = 0;
+    for (size_t i = 0; i < free_.size();)
+      if (free_[i]->cap < cap) {
+        ++*n;
+        *bytes += free_[i]->cap;
+        release(free_[i]);
+        free_.erase(free_.begin() + (long)i);
+      } else {
+        ++i;
+      }
+  }
   std::shared_ptr<TextBuf> get(size_t cap) {
     TextBuf *b = nullptr;
     {
@@ -464,6 +486,60 @@ int formatOf(const char *path) {
   throw std::runtime_error(std::string("Unsupported file type: ") + path);
 }
 
+// The first record start at or after byte x of a plain read file of `size` bytes (size when none):
+// FASTA, a line starting with '>'; FASTQ, a line starting with '@' whose next-but-one line starts
+// with '+'.  The FASTQ test is unique: a quality line may start with '@', but two lines below it is
+// the next record's sequence line (or header), never a '+' line; sequence lines start with neither.
+// A record found this way is one the sequential framing (frameRecords) starts as well.
+uint64_t syncRecord(int fd, uint64_t size, uint64_t x, int fmt) {
+  if (x == 0 || x >= size) return x >= size ? size : 0;
+  uint64_t win = 1ull << 20;
+  for (;;) {
+    const uint64_t a = x - 1, b = std::min(size, a + win);
+    std::string t(b - a, '\0');
+    uint64_t got = 0;
+    while (got < t.size()) {
+      const ssize_t r = ::pread(fd, &t[got], t.size() - got, (off_t)(a + got));
+      if (r <= 0) throw std::runtime_error("read error while locating a shard boundary");
+      got += (uint64_t)r;
+    }
+    const bool atEnd = b == size;
+    // line starts from x on: x itself when byte x - 1 ends a line
+    size_t p = 1;
+    if (t[0] != '\n') {
+      const size_t nl = t.find('\n', 1);
+      if (nl == std::string::npos) {
+        if (atEnd) return size;
+        win *= 4;
+        continue;
+      }
+      p = nl + 1;
+    }
+    bool more = false;
+    while (p < t.size()) {
+      if (fmt == 0 ? t[p] == '>' : t[p] == '@') {
+        if (fmt == 0) return a + p;
+        const size_t n1 = t.find('\n', p), n2 = n1 == std::string::npos ? n1 : t.find('\n', n1 + 1);
+        if (n2 == std::string::npos || n2 + 1 >= t.size()) {
+          if (atEnd) return size;  // no complete record follows
+          more = true;
+          break;
+        }
+        if (t[n2 + 1] == '+') return a + p;
+      }
+      const size_t nl = t.find('\n', p);
+      if (nl == std::string::npos) {
+        if (atEnd) return size;
+        more = true;
+        break;
+      }
+      p = nl + 1;
+    }
+    if (!more && atEnd) return size;
+    win *= 4;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -561,7 +637,40 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
   }
 }
 
+int gwa_reads_shard_range(const char *path, uint32_t shard, uint32_t nshards, uint64_t *begin, uint64_t *end) {
+  int in = -1;
+  try {
+    if (nshards == 0 || shard >= nshards) throw std::runtime_error("shard index out of range");
+    const int fmt = formatOf(path);
+    if (strlen(path) > 3 && strcmp(path + strlen(path) - 3, ".gz") == 0)
+      throw std::runtime_error(std::string("a sharded run needs an uncompressed read file (not .gz): ") + path);
+    in = ::open(path, O_RDONLY);
+    if (in < 0) throw std::runtime_error(std::string("cannot open ") + path);
+    struct stat st;
+    if (::fstat(in, &st) != 0 || !S_ISREG(st.st_mode))
+      throw std::runtime_error(std::string("a sharded run needs a regular read file: ") + path);
+    const uint64_t size = (uint64_t)st.st_size;
+    auto cut = [&](uint64_t s) -> uint64_t {
+      if (s == 0) return 0;
+      if (s >= nshards) return size;
+      return syncRecord(in, size, (uint64_t)((unsigned __int128)size * s / nshards), fmt);
+    };
+    *begin = cut(shard);
+    *end = cut(shard + 1);
+    ::close(in);
+    return 0;
+  } catch (std::exception &e) {
+    if (in >= 0) ::close(in);
+    return gwa_fail_message(e.what());
+  }
+}
+
 int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_t *n_reads) {
+  return gwa_pipeline_align_file_range(p, path, fd, 0, ~0ull, n_reads);
+}
+
+int gwa_pipeline_align_file_range(gwa_pipeline_t *p, const char *path, int fd, uint64_t begin, uint64_t end,
+                                  uint64_t *n_reads) {
   BufPool &pool = p->pool;
   Run run(p);
   gzFile f = nullptr;
@@ -569,13 +678,19 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
   try {
     const int fmt = formatOf(path);
     const bool gz = strlen(path) > 3 && strcmp(path + strlen(path) - 3, ".gz") == 0;
+    const bool whole = begin == 0 && end == ~0ull;
     if (gz) {
+      if (!whole) throw std::runtime_error(std::string("a byte range needs an uncompressed read file: ") + path);
       f = gzopen(path, "rb");
       if (!f) throw std::runtime_error(std::string("cannot open ") + path);
       gzbuffer(f, 1u << 20);
     } else {
       in = ::open(path, O_RDONLY);
       if (in < 0) throw std::runtime_error(std::string("cannot open ") + path);
+      struct stat st;
+      if (::fstat(in, &st) == 0 && S_ISREG(st.st_mode)) end = std::min<uint64_t>(end, (uint64_t)st.st_size);
+      if (begin > end) begin = end;
+      if (::lseek(in, (off_t)begin, SEEK_SET) < 0) throw std::runtime_error(std::string("cannot seek in ") + path);
     }
     struct stat sb;
     const off_t pos0 = ::lseek(fd, 0, SEEK_CUR);
@@ -589,7 +704,7 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
     uint64_t fileBytes = 0;
     {
       struct stat st;
-      if (!gz && ::fstat(in, &st) == 0 && S_ISREG(st.st_mode)) fileBytes = (uint64_t)st.st_size;
+      if (!gz && ::fstat(in, &st) == 0 && S_ISREG(st.st_mode)) fileBytes = end - begin;
     }
     const uint64_t chunk = fileBytes ? std::min<uint64_t>(kChunk, ((fileBytes >> 20) + 1) << 20) : kChunk;
     const uint64_t reserve = std::min<uint64_t>(kReserve, 2 * chunk);
@@ -598,18 +713,29 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
     // the runtime (measured: FASTQ -> SAM 8 M reads/s with background pinning, 20-25 M with the
     // buffers pinned first) -- as many as the file needs, at most a quarter of the available host
     // memory, kept for later calls.  Beyond them runs use pageable buffers.
+    uint64_t pinnedUsable = 0;
+    // Buffers pinned by an earlier call for a smaller file cannot hold this file's chunks: they are
+    // unpinned, and only the pinned buffers of at least reserve + chunk bytes count.
     {
       const uint64_t nbuf = 4 + (uint64_t)p->ix.size() * (uint64_t)p->workersPerDevice;
       const uint64_t need = fileBytes ? std::min<uint64_t>(nbuf, fileBytes / chunk + 3) : nbuf;
       const uint64_t avail = memAvailable(), capB = avail ? avail / 4 : (8ull << 30);
+      const uint64_t bufCap = reserve + chunk;
+      uint64_t relN = 0, relB = 0;
+      p->pool.releasePinnedBelow(bufCap, &relN, &relB);
+      p->pinnedBufs -= std::min(p->pinnedBufs, relN);
+      p->pinnedBytes -= std::min(p->pinnedBytes, relB);
+      uint64_t usable = p->pool.countPinned(bufCap);
       try {
-        while (p->pinnedBufs < need && p->pinnedBytes + reserve + chunk <= capB) {
-          p->pool.addPinned(reserve + chunk);
+        while (usable < need && p->pinnedBytes + bufCap <= capB) {
+          p->pool.addPinned(bufCap);
           ++p->pinnedBufs;
-          p->pinnedBytes += reserve + chunk;
+          ++usable;
+          p->pinnedBytes += bufCap;
         }
       } catch (std::exception &) {  // (pinning failed: pageable buffers)
       }
+      pinnedUsable = usable;
     }
     const auto t0 = Clock::now();
     double readS = 0, frameS = 0;
@@ -651,17 +777,19 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
               if (r == 0) break;
               c.got += (uint64_t)r;
             }
-          } else {  // four preads at a time (the page cache copies in parallel)
+          } else {  // four preads at a time (the page cache copies in parallel), up to `end`
             const off_t at = ::lseek(in, 0, SEEK_CUR);
+            const uint64_t want = std::min<uint64_t>(chunk, end > (uint64_t)at ? end - (uint64_t)at : 0);
             std::atomic<bool> bad{false};
             std::vector<std::thread> th;
-            const uint64_t part = chunk / 4;
             std::vector<uint64_t> gotk(4, 0);
+            auto lo = [&](int k) { return want * (uint64_t)k / 4; };
             for (int k = 0; k < 4; ++k)
               th.emplace_back([&, k] {
+                const uint64_t part = lo(k + 1) - lo(k);
                 uint64_t gk = 0;
                 while (gk < part) {
-                  const ssize_t r = ::pread(in, dst + k * part + gk, (size_t)(part - gk), at + (off_t)(k * part + gk));
+                  const ssize_t r = ::pread(in, dst + lo(k) + gk, (size_t)(part - gk), at + (off_t)(lo(k) + gk));
                   if (r < 0) { bad = true; return; }
                   if (r == 0) break;
                   gk += (uint64_t)r;
@@ -673,11 +801,12 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
             // the bytes read are contiguous up to the first short part (end of file)
             for (int k = 0; k < 4; ++k) {
               c.got += gotk[(size_t)k];
-              if (gotk[(size_t)k] < part) break;
+              if (gotk[(size_t)k] < lo(k + 1) - lo(k)) break;
             }
             ::lseek(in, at + (off_t)c.got, SEEK_SET);
+            if ((uint64_t)at + c.got >= end) c.got = std::min<uint64_t>(c.got, end - (uint64_t)at);
           }
-          c.final = c.got < chunk;
+          c.final = c.got < chunk || (!gz && (uint64_t)::lseek(in, 0, SEEK_CUR) >= end);
           const double rs = secs(r0, Clock::now());
           std::lock_guard<std::mutex> g(qmu);
           readS += rs;
@@ -841,6 +970,7 @@ int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_
     st = gwa_pipeline_stats_t{};
     st.reads = n;
     st.batches = run.fileBatches;
+    st.pinned_bufs = pinnedUsable;
     st.wall_s = secs(t0, Clock::now());
     st.read_s = readS;
     st.frame_s = frameS;

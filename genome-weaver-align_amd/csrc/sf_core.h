@@ -27,8 +27,8 @@ struct SfState {
 static_assert(sizeof(SfState<4>) <= sizeof(DState<4>), "SfState must fit the DState arena slots");
 
 template <int R, int QW>
-struct SfLane : BsfLane<R, QW> {
-  typedef BsfLane<R, QW> B;
+struct SfLane : BsfLane<R, QW, false, 24> {
+  typedef BsfLane<R, QW, false, 24> B;
   using B::ix;
   using B::cfg;
   using B::L;
@@ -54,16 +54,70 @@ struct SfLane : BsfLane<R, QW> {
   GWA_HD SfState<R> *arena() const { return (SfState<R> *)L.slice; }
   int nCand = 0;  // candidates (TreeSet<Long>[2], :295) as start << 1 | strand in L.cand()
 
+  // A polled SFState is never read again (the loop works on its register copy; SF has no split
+  // chains), so its arena slot is recycled: the arena holds the queued states only, and its size
+  // bounds the live queue, not the states created.  Free slots are linked through SfState::lb.
+  int freeHead = -1, created = 0;
+  GWA_HD int sfAlloc() {
+    if (freeHead >= 0) {
+      const int id = freeHead;
+      freeHead = (int)arena()[id].lb;
+      return id;
+    }
+    return B::allocState();
+  }
+  GWA_HD void sfFree(int id) {
+    arena()[id].lb = (uint32_t)freeHead;
+    freeHead = id;
+  }
+
+  // candidates[strand].contains(start) / add: a linear scan of L.cand() for the small sets of the
+  // first tiers; an open-addressing hash table (caps.cand slots, a power of two, at most half full)
+  // when caps.cand >= kCandHash -- the deep tiers hold reads with tens of thousands of candidates,
+  // where a scan per candidate would be quadratic.  Only membership is used (:304-306), so the
+  // table's order does not matter.
+  static constexpr int kCandHash = 4096;
+  static constexpr int64_t kCandEmpty = (int64_t)0x8000000000000000LL;
+  GWA_HD void candClear() {
+    nCand = 0;
+    if (caps.cand >= kCandHash)
+      for (int i = 0; i < caps.cand; ++i) L.cand()[i] = kCandEmpty;
+  }
+  // 1 = newly added, 0 = already present, -1 = the set is full (overflow)
+  GWA_HD int candInsert(int64_t key) {
+    int64_t *c = L.cand();
+    if (caps.cand < kCandHash) {
+      for (int i = 0; i < nCand; ++i)
+        if (c[i] == key) return 0;
+      if (nCand >= caps.cand) return -1;
+      c[nCand++] = key;
+      return 1;
+    }
+    const uint32_t mask = (uint32_t)caps.cand - 1u;
+    uint32_t h = (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ULL) >> 40) & mask;
+    for (;;) {
+      const int64_t v = c[h];
+      if (v == key) return 0;
+      if (v == kCandEmpty) break;
+      h = (h + 1u) & mask;
+    }
+    if (2 * (nCand + 1) > caps.cand) return -1;
+    c[h] = key;
+    ++nCand;
+    return 1;
+  }
+
   // SFState.compareTo (:463-469) as a heap key: kOffset ascending, then score descending
   GWA_HD static uint64_t keyOf(int kOffset, int score) {
     return ((uint64_t)(kOffset & 0xFF) << 32) | ((uint64_t)((int64_t)0x7FFFFFFF - (int64_t)score) & 0xFFFFFFFFULL);
   }
-  GWA_HD void push(int idx, int kOffset, int score) { B::queueAddKeyed((keyOf(kOffset, score) << 16) | (uint64_t)idx); }
+  GWA_HD void push(int idx, int kOffset, int score) { B::queueAddKeyed((keyOf(kOffset, score) << 24) | (uint64_t)idx); }
 
   GWA_HD int newState(int strand, int offset, int index, int score, uint32_t lb, uint32_t ub, uint8_t meta,
                       const uint64_t (&rows)[R], int nrows, int kOffset, bool hasHit) {
-    const int id = B::allocState();
+    const int id = sfAlloc();
     if (id < 0) return -1;
+    ++created;
     SfState<R> d;
     d.lb = lb; d.ub = ub; d.score = score;
     d.strand = (uint8_t)strand; d.offset = (uint8_t)offset; d.index = (uint8_t)index; d.nrows = (uint8_t)nrows;
@@ -197,7 +251,7 @@ struct SfLane : BsfLane<R, QW> {
       if (L.hits()[e].diff <= minMismatches) L.list()[n++] = e;
     }
     if (n >= caps.list) {
-      status = ST_OVERFLOW;
+      B::ovf(OV_LIST);
       listSize = n;
       return;
     }
@@ -222,13 +276,12 @@ struct SfLane : BsfLane<R, QW> {
     const int offsetFromSearchHead = strand == 0 ? c.index : m - c.index;
     const int64_t start = seqIndex - offsetFromSearchHead;
     const int64_t key = (int64_t)((uint64_t)start << 1) | strand;
-    for (int i = 0; i < nCand; ++i)
-      if (L.cand()[i] == key) return true;  // candidates[strand].contains(start)
-    if (nCand >= caps.cand) {
-      status = ST_OVERFLOW;
+    const int ins = candInsert(key);
+    if (ins == 0) return true;  // candidates[strand].contains(start)
+    if (ins < 0) {
+      B::ovf(OV_CAND);
       return false;
     }
-    L.cand()[nCand++] = key;
     const int64_t refStart = start - k > 0 ? start - k : 0;
     const int64_t refEnd = start + m + k < (int64_t)ix.N ? start + m + k : (int64_t)ix.N;
     if (refStart > refEnd) {  // ACGTSequence.subString throws
@@ -275,6 +328,7 @@ struct SfLane : BsfLane<R, QW> {
     if (heapSize == 0 || status == ST_OVERFLOW || status == ST_ERROR) return false;
     const int idx = B::queuePoll();
     const SfState<R> c = arena()[idx];
+    sfFree(idx);
     const int ubScore = c.score + (c.offset + (m - c.index)) * cfg.matchScore;  // scoreUpperBound (:444-446)
     if ((int)c.kOffset > minMismatches || ubScore < bestScore) return true;    // numCutOff++
     if (c.hasHit || c.index >= m || c.ub - c.lb == 1) return addCandidate(c);
@@ -291,7 +345,9 @@ struct SfLane : BsfLane<R, QW> {
   }
 
   GWA_HD void sfSearch() {
-    nCand = 0;
+    candClear();
+    freeHead = -1;
+    created = 0;
     if (!sfStart()) return;
     while (sfStep()) {
     }

@@ -66,24 +66,32 @@ def gather_sam(sam_text, dst=0):
 
 def gather_sam_device(sam, dst=0):
     """Gather each rank's SAM text held in a uint8 tensor (on the GPU with the nccl backend = RCCL over
-    xGMI, or on the CPU with gloo) to `dst`, concatenated in rank order = input order: one all-gather
-    of the lengths, then one all-gather of the texts padded to the longest (RCCL's gather is built
-    from point-to-point sends; a ring all-gather keeps every xGMI link busy).  Returns the merged
-    uint8 tensor on `dst`, None on the other ranks; the tensor itself without torch.distributed."""
+    xGMI, or on the CPU with gloo) to `dst`, concatenated in rank order = input order.  One all-gather
+    of the lengths (8 bytes per rank), then every other rank sends its text once, point to point, into
+    its slice of the merged buffer on `dst`: each text crosses the fabric once and no rank but `dst`
+    holds more than its own (an all-gather of padded texts would move N x the data into every rank).
+    Returns the merged uint8 tensor on `dst`, None on the other ranks; the tensor itself without
+    torch.distributed."""
     import torch
     import torch.distributed as td
     if not (td.is_available() and td.is_initialized()) or td.get_world_size() == 1:
         return sam
-    w = td.get_world_size()
+    w, me = td.get_world_size(), td.get_rank()
+    sam = sam.contiguous().view(-1)
     n = torch.tensor([sam.numel()], dtype=torch.int64, device=sam.device)
     lens = [torch.zeros_like(n) for _ in range(w)]
     td.all_gather(lens, n)
     lens = [int(x.item()) for x in lens]
-    top = max(lens)
-    buf = torch.zeros(top, dtype=torch.uint8, device=sam.device)
-    buf[:sam.numel()] = sam
-    parts = [torch.empty(top, dtype=torch.uint8, device=sam.device) for _ in range(w)]
-    td.all_gather(parts, buf)
-    if td.get_rank() != dst:
+    if me != dst:
+        if lens[me]:
+            td.send(sam, dst)
         return None
-    return torch.cat([p[:l] for p, l in zip(parts, lens)])
+    out = torch.empty(sum(lens), dtype=torch.uint8, device=sam.device)
+    off = 0
+    for r, ln in enumerate(lens):
+        if r == dst:
+            out[off:off + ln].copy_(sam)
+        elif ln:
+            td.recv(out[off:off + ln], src=r)
+        off += ln
+    return out

@@ -62,11 +62,20 @@ class BatchStats(ctypes.Structure):
                 ("rescue_ms", ctypes.c_double), ("heavy_pairs", ctypes.c_uint64)]
 
 
+def shard_range(path, shard, nshards):
+    """Byte range [begin, end) of contiguous shard `shard` of `nshards` of a plain read file, cut at record
+    starts (include/gwa.h gwa_reads_shard_range): the shards' SAM concatenated in order is a one-process
+    run's SAM."""
+    b, e = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().gwa_reads_shard_range(path.encode(), shard, nshards, ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
 class PipelineStats(ctypes.Structure):
     _fields_ = [("reads", ctypes.c_uint64), ("batches", ctypes.c_uint64), ("wall_s", ctypes.c_double),
                 ("read_s", ctypes.c_double), ("device_kernel_s", ctypes.c_double * 16), ("parse_s", ctypes.c_double),
                 ("setup_s", ctypes.c_double), ("format_s", ctypes.c_double), ("write_s", ctypes.c_double),
-                ("order_wait_s", ctypes.c_double), ("frame_s", ctypes.c_double)]
+                ("order_wait_s", ctypes.c_double), ("frame_s", ctypes.c_double), ("pinned_bufs", ctypes.c_uint64)]
 
 
 _lib = None
@@ -78,7 +87,8 @@ EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_inde
            "gwa_batch_create", "gwa_batch_create_pairs", "gwa_align_pairs", "gwa_batch_run", "gwa_batch_stats", "gwa_batch_results", "gwa_batch_free",
            "gwa_batch_read_counters", "gwa_batch_results_range", "gwa_results_records", "gwa_batch_results_select", "gwa_batch_format",
            "gwa_batch_sam_copy",
-           "gwa_pipeline_open", "gwa_pipeline_align", "gwa_pipeline_align_file", "gwa_pipeline_stats",
+           "gwa_pipeline_open", "gwa_pipeline_align", "gwa_pipeline_align_file", "gwa_pipeline_align_file_range",
+           "gwa_reads_shard_range", "gwa_pipeline_stats",
            "gwa_pipeline_close", "gwa_reads_parse", "gwa_reads_free"]
 
 
@@ -123,6 +133,8 @@ def lib():
         L.gwa_pipeline_open.argtypes = [V, I, P(_Config), ctypes.c_uint32, I, P(V)]
         L.gwa_pipeline_align.argtypes = [V, P(_Reads), P(_Results)]
         L.gwa_pipeline_align_file.argtypes = [V, ctypes.c_char_p, I, P(U64)]
+        L.gwa_pipeline_align_file_range.argtypes = [V, ctypes.c_char_p, I, U64, U64, P(U64)]
+        L.gwa_reads_shard_range.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, P(U64), P(U64)]
         L.gwa_pipeline_stats.argtypes = [V, P(PipelineStats)]
         L.gwa_pipeline_close.argtypes = [V]
         _lib = L
@@ -455,10 +467,15 @@ class Pipeline:
         _check(lib().gwa_pipeline_align(self.h, ctypes.byref(reads_struct), ctypes.byref(res)))
         return _take_results(res)[0]
 
-    def align_file(self, path, fd):
-        """Stream a FASTA/FASTQ[.gz] read file through the devices; SAM records to file descriptor fd."""
+    def align_file(self, path, fd, shard=None):
+        """Stream a FASTA/FASTQ[.gz] read file through the devices; SAM records to file descriptor fd.
+        shard=(r, N): only the records of contiguous shard r of N (a plain file; shard_range)."""
         n = ctypes.c_uint64()
-        _check(lib().gwa_pipeline_align_file(self.h, path.encode(), fd, ctypes.byref(n)))
+        if shard is None:
+            _check(lib().gwa_pipeline_align_file(self.h, path.encode(), fd, ctypes.byref(n)))
+        else:
+            b, e = shard_range(path, *shard)
+            _check(lib().gwa_pipeline_align_file_range(self.h, path.encode(), fd, b, e, ctypes.byref(n)))
         return n.value
 
     def stats(self):
@@ -500,6 +517,7 @@ class Batch:
         (mate-1 blobs, mate-2 blobs) makes a paired-end batch (gwa_batch_create_pairs)."""
         self._keep = []
         self.h = ctypes.c_void_p()
+        self.device = fmIndex.device  # the GPU holding the batch (its index's)
         c = config._c()
         if pair_blobs is not None:
             self._keep.append(pair_blobs)
@@ -538,7 +556,7 @@ class Batch:
         import torch
         n = ctypes.c_uint64()
         _check(lib().gwa_batch_sam_copy(self.h, None, ctypes.byref(n)))
-        t = torch.empty(n.value, dtype=torch.uint8, device="cuda")
+        t = torch.empty(n.value, dtype=torch.uint8, device=torch.device("cuda", self.device))
         if n.value:
             _check(lib().gwa_batch_sam_copy(self.h, ctypes.c_void_p(t.data_ptr()), ctypes.byref(n)))
         return t

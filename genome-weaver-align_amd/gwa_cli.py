@@ -124,7 +124,24 @@ def build_parser():
     a.add_argument("--timing", action="store_true", help="index / align wall times and reads/s on stderr")
     a.add_argument("--insert-min", type=int, default=210, help="paired-end: smallest template length of a proper pair")
     a.add_argument("--insert-max", type=int, default=390, help="paired-end: largest template length of a proper pair")
+    a.add_argument("--shard", default=None, metavar="R/N",
+                   help="one process per GPU: align contiguous shard R of N of the (plain) read file; the SAM "
+                        "header is written by shard 0 only, so the shards' outputs concatenated in order are "
+                        "the one-process SAM")
     return ap
+
+
+def shard_of(ns):
+    """--shard R/N as (R, N), or None"""
+    if ns.shard is None:
+        return None
+    try:
+        r, n = (int(x) for x in ns.shard.split("/"))
+    except ValueError:
+        raise gwa.GwaError("--shard takes R/N (e.g. 0/8), got %r" % ns.shard)
+    if n < 1 or not 0 <= r < n:
+        raise gwa.GwaError("--shard %s: need 0 <= R < N" % ns.shard)
+    return r, n
 
 
 def config_of(ns):
@@ -174,15 +191,21 @@ def align(ns, out=sys.stdout):
     if ns.query is None and len(ns.readFiles) not in (1, 2):
         raise gwa.GwaError("give one read file (single-end) or two mate files (paired-end)")
     cfg = config_of(ns)
+    shard = shard_of(ns)
+    if shard is not None and (ns.query is not None or len(ns.readFiles) != 1):
+        raise gwa.GwaError("--shard splits one single-end read file")
     if ns.query is None:
         for f in ns.readFiles:
             _kind(f)  # unsupported suffixes fail before the index is built
+    if shard is not None:
+        gwa.shard_range(ns.readFiles[0], *shard)  # (a .gz or missing file fails before the index is built)
     devices = [int(x) for x in ns.devices.split(",")] if ns.devices else [ns.device]
     t0 = time.perf_counter()
     fms = load_indexes(ns.refSeq, devices)
     t1 = time.perf_counter()
     w = (lambda s: None) if ns.silent else out.write
-    w(fms[0].samHeader())
+    if shard is None or shard[0] == 0:
+        w(fms[0].samHeader())
     n = 0
     t_open = 0.0
     try:
@@ -199,14 +222,14 @@ def align(ns, out=sys.stdout):
             try:
                 if ns.silent:
                     with open(os.devnull, "wb") as dn:
-                        n = pipe.align_file(ns.readFiles[0], dn.fileno())
+                        n = pipe.align_file(ns.readFiles[0], dn.fileno(), shard=shard)
                 else:
                     try:
                         fd = out.fileno()
                     except (AttributeError, io.UnsupportedOperation):
                         fd = None
                     if fd is not None:
-                        n = pipe.align_file(ns.readFiles[0], fd)
+                        n = pipe.align_file(ns.readFiles[0], fd, shard=shard)
                         if ns.timing:
                             st = pipe.stats()
                             print("[gwa] pipeline %.2fs: read %.2fs, frame %.2fs; summed over %d worker threads: parse %.2fs, "
@@ -216,7 +239,7 @@ def align(ns, out=sys.stdout):
                                      st.format_s, st.write_s, st.order_wait_s), file=sys.stderr)
                     else:  # an in-memory stream (tests): through a temporary file
                         with tempfile.TemporaryFile() as tf:
-                            n = pipe.align_file(ns.readFiles[0], tf.fileno())
+                            n = pipe.align_file(ns.readFiles[0], tf.fileno(), shard=shard)
                             tf.seek(0)
                             out.write(tf.read().decode())
             finally:

@@ -220,6 +220,7 @@ typedef struct {
    * SAM formatting + D2H, output writes, and waiting for the batch-order output position */
   double parse_s, setup_s, format_s, write_s, order_wait_s;
   double frame_s;  /* reader thread: framing the text into batches of complete records */
+  uint64_t pinned_bufs;  /* align_file: pinned read-text buffers large enough for this file's chunks */
 } gwa_pipeline_stats_t;
 int gwa_pipeline_open(gwa_index_t *const *ix, int n_ix, const gwa_config_t *cfg, uint32_t batch_reads,
                       int workers_per_device, gwa_pipeline_t **out);
@@ -229,6 +230,15 @@ int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_
  * R/ReadReaderFactory.java:126-151) streamed through the devices; SAM records (no header) are
  * written to fd in input order.  *n_reads = reads aligned. */
 int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_t *n_reads);
+/* The same over the bytes [begin, end) of a plain (not .gz) read file, which must start at a record
+ * (gwa_reads_shard_range gives such ranges). */
+int gwa_pipeline_align_file_range(gwa_pipeline_t *p, const char *path, int fd, uint64_t begin, uint64_t end,
+                                  uint64_t *n_reads);
+/* One process per GPU (C3; the reference's one read loop, A/Align.java:174-196, split by reads): the
+ * byte range [*begin, *end) of shard `shard` of `nshards` contiguous shards of a plain FASTQ / FASTA
+ * file, cut at record starts, so that the shards' SAM files concatenated in shard order equal a
+ * one-process run's (the header belongs to shard 0). */
+int gwa_reads_shard_range(const char *path, uint32_t shard, uint32_t nshards, uint64_t *begin, uint64_t *end);
 int gwa_pipeline_stats(const gwa_pipeline_t *p, gwa_pipeline_stats_t *st);
 void gwa_pipeline_close(gwa_pipeline_t *p);
 

@@ -295,3 +295,120 @@ def test_pipeline_appends_in_input_order(tmp_path):
     oi = O.Index.from_fasta(ref.read_text())
     sam = oi.align(reads, O.OrcConfig.default(k=2.0))
     assert out.read_text() == "@HD\tVN:1.0\n" + sam + sam
+
+
+# ---- --shard R/N: contiguous shards of one read file (one process per GPU, C3) ----
+
+def _tricky_fastq(n, seed=5):
+    """FASTQ whose quality lines often start with '@' or '+' (the shard cut must not sync on them),
+    with blank lines, CRLF records and empty reads mixed in"""
+    import random
+    rnd = random.Random(seed)
+    out = []
+    for i in range(n):
+        m = rnd.choice([0, 1, 7, 60, 100, 151])
+        seq = "".join(rnd.choice("ACGTN") for _ in range(m))
+        qual = "".join(rnd.choice("@+!#IJ5") for _ in range(m))
+        if m and rnd.random() < 0.4:
+            qual = rnd.choice("@+") + qual[1:]
+        eol = "\r\n" if rnd.random() < 0.1 else "\n"
+        out.append("@r%d x%s%s%s+%s%s%s" % (i, eol, seq, eol, eol, qual, eol))
+        if rnd.random() < 0.05:
+            out.append("\n")
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("fmt", ["fq", "fa"])
+def test_shard_ranges_tile_the_file_at_record_starts(tmp_path, fmt):
+    # gwa_reads_shard_range (host code only): for every shard count the ranges tile the file, each
+    # starts at a record, and the records of the shards in order are the file's records
+    if fmt == "fq":
+        text = _tricky_fastq(3000)
+    else:
+        import random
+        rnd = random.Random(9)
+        text = "".join(">s%d d\n%s\n%s\n" % (i, "".join(rnd.choice("ACGT>") for _ in range(rnd.randint(1, 70))).replace(">", "A"),
+                                             "ACGT" * rnd.randint(0, 9)) for i in range(2000)).encode()
+    p = tmp_path / ("reads." + fmt)
+    p.write_bytes(text)
+    whole = _native_records(text, "fastq" if fmt == "fq" else "fasta", 1 << 30)
+    assert len(whole) == (3000 if fmt == "fq" else 2000)
+    for nsh in (1, 2, 3, 7, 16, 64):
+        ranges = [gwa.shard_range(str(p), r, nsh) for r in range(nsh)]
+        assert ranges[0][0] == 0 and ranges[-1][1] == len(text)
+        assert all(ranges[i][1] == ranges[i + 1][0] for i in range(nsh - 1))
+        got = []
+        for b, e in ranges:
+            part = text[b:e]
+            if part:
+                assert part[:1] == (b"@" if fmt == "fq" else b">")
+            got += _native_records(part, "fastq" if fmt == "fq" else "fasta", 1 << 30)
+        assert got == whole, nsh
+
+
+def test_shard_options_and_errors(tmp_path):
+    p = tmp_path / "r.fq.gz"
+    with gzip.open(p, "wt") as f:
+        f.write("@a\nACGT\n+\nIIII\n")
+    with pytest.raises(gwa.GwaError, match="uncompressed"):
+        gwa.shard_range(str(p), 0, 2)
+    q = tmp_path / "r.fq"
+    q.write_text("@a\nACGT\n+\nIIII\n")
+    with pytest.raises(gwa.GwaError):
+        gwa.shard_range(str(q), 2, 2)
+    assert gwa.shard_range(str(q), 1, 2)[1] == q.stat().st_size
+    for bad in ("3", "2/2", "a/b", "-1/2"):
+        ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "--shard=" + bad, str(q)])
+        with pytest.raises(gwa.GwaError):
+            gwa_cli.shard_of(ns)
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", "ref.fa", "--shard", "1/4", str(q)])
+    assert gwa_cli.shard_of(ns) == (1, 4)
+
+
+@pytest.mark.gpu
+def test_cli_shards_concatenate_to_the_one_process_sam(tmp_path):
+    # `align --shard r/N` for every r: the outputs concatenated in shard order are byte-identical to
+    # one run over the whole file (header from shard 0 only), and to the oracle
+    import oracle as O
+    ref, rp, reads = _e2e_inputs(tmp_path, "fq", n=4000, cid=18)
+    one = io.StringIO()
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-k", "2", "--batch", "300", str(rp)])
+    assert gwa_cli.align(ns, out=one) == len(reads)
+    for nsh in (2, 5):
+        parts, total = [], 0
+        for r in range(nsh):
+            out = tmp_path / ("shard%d_%d.sam" % (nsh, r))
+            with open(out, "w") as f:
+                ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-k", "2", "--batch", "300",
+                                                        "--shard", "%d/%d" % (r, nsh), str(rp)])
+                total += gwa_cli.align(ns, out=f)
+            parts.append(out.read_text())
+        assert total == len(reads)
+        assert "".join(parts) == one.getvalue()
+    oi = O.Index.from_fasta(ref.read_text())
+    assert one.getvalue() == oi.sam_header() + oi.align(reads, O.OrcConfig.default(k=2.0))
+
+
+@pytest.mark.gpu
+def test_pipeline_small_file_then_large_file_pins_for_the_large_one(tmp_path):
+    # a pipeline that first aligns a small file pins small read-text buffers; a later large file must
+    # not run on pageable memory because of them (they are unpinned and replaced by buffers of the
+    # large file's chunk size); results stay identical
+    ref, small, _ = _e2e_inputs(tmp_path, "fq", n=300, cid=19)
+    big = tmp_path / "big.fq"
+    rec = small.read_bytes()
+    with open(big, "wb") as f:  # > 2 chunks of kChunk = 256 MiB is too slow here: the rule is per size
+        for _ in range(200):
+            f.write(rec)
+    fm = gwa.FMIndexOnGenome.load(str(ref))
+    pipe = gwa.Pipeline([fm], gwa.AlignmentConfig(k=2.0), batch_reads=4096, workers_per_device=2)
+    with open(tmp_path / "a.sam", "wb") as f:
+        pipe.align_file(str(small), f.fileno())
+    n_small = pipe.stats().pinned_bufs
+    with open(tmp_path / "b.sam", "wb") as f:
+        pipe.align_file(str(big), f.fileno())
+    st = pipe.stats()
+    pipe.close()
+    fm.close()
+    assert n_small >= 3 and st.pinned_bufs >= 3
+    assert (tmp_path / "b.sam").read_bytes() == (tmp_path / "a.sam").read_bytes() * 200

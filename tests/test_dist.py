@@ -92,3 +92,27 @@ def test_two_rank_shard_gather_equals_single(tmp_path):
     m0, d0 = map(float, open(tmp_path / "max.txt").read().split())
     m1, d1 = map(float, open(tmp_path / "rank1.txt").read().split())
     assert m0 == m1 == max(d0, d1)
+
+
+def _gather_main(rank, world_size, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world_size))
+    import torch
+    import torch.distributed as td
+    td.init_process_group("gloo", rank=rank, world_size=world_size)
+    # uneven texts, one rank with none: each rank sends its own bytes once, rank 0 merges in rank order
+    text = b"" if rank == 1 else (b"rank%d line\n" % rank) * (1000 * (rank + 1))
+    out = dist.gather_sam_device(torch.frombuffer(bytearray(text), dtype=torch.uint8) if text
+                                 else torch.empty(0, dtype=torch.uint8))
+    if rank == 0:
+        with open(os.path.join(outdir, "g.bin"), "wb") as f:
+            f.write(out.numpy().tobytes())
+    else:
+        assert out is None
+    td.barrier()
+    td.destroy_process_group()
+
+
+def test_three_rank_point_to_point_gather(tmp_path):
+    mp.start_processes(_gather_main, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True, start_method="spawn")
+    exp = b"".join(b"" if r == 1 else (b"rank%d line\n" % r) * (1000 * (r + 1)) for r in range(3))
+    assert (tmp_path / "g.bin").read_bytes() == exp
