@@ -186,8 +186,8 @@ struct DState {
   uint32_t bBase;         // SI_BID: B interval of ch = bBase + sum_{j<ch} width_j + [0, width_ch)
   int32_t state;          // flags(5) | base(3) | minK(8) | priority(8) | hasHit(1) | clipped(1)  (:664)
   int32_t nextSplit;      // arena index, -1 = null
-  uint8_t flag, start, end, cursor;  // Cursor (S/Cursor.java:42-47)
-  uint8_t pivot, nrows, kOffset, meta;
+  uint8_t flag, nrows, kOffset, meta;
+  uint16_t start, end, cursor, pivot;  // Cursor (S/Cursor.java:42-47); reads up to 512 bp
   uint64_t nfa[R];        // ReadAlignmentNFA rows (S/ReadAlignmentNFA.java:60-61)
 };
 
@@ -356,9 +356,9 @@ struct Overflow {};  // thrown only on host test builds; device uses status code
 
 // QW = 2-bit query words per strand held in registers (4: reads <= 128 bp, 8: <= 255 bp); the
 // DP then needs at most DB = QW / 2 blocks of 64 rows.  HY: hybrid heap (hslot).
-// KS: bits of the state index in a queue entry (key << KS | index): 16 on the BSF path (its 48-bit
-// key; arenas <= 65536 states), 24 on the SF path (40-bit key; arenas up to 2^24 states).
-template <int R, int QW = 8, bool HY = false, int KS = 16>
+// KS: bits of the state index in a queue entry (key << KS | index).  Both paths' keys are 40 bits
+// (packKey here, SfLane::keyOf), so an arena holds up to 2^24 states.
+template <int R, int QW = 8, bool HY = false, int KS = 24>
 struct BsfLane {
   static constexpr int DB = QW / 2;
   static constexpr uint64_t IDXM = (1ULL << KS) - 1ULL;
@@ -651,12 +651,42 @@ struct BsfLane {
   // global access).
   lds_cu64 *stairLds = nullptr;
   const uint64_t *stairTab = nullptr;
-  int stairBad = 0, stairInLds = 0;
+  uint64_t stairBad = 0;  // bit kk: StaircaseFilter(m, kk) throws (the reference's (byte) chunk starts)
+  int stairInLds = 0;
+  // getStairCaseFilter(m) (S/BidirectionalSuffixFilter.java:206-208, S/SuffixFilter.java:140-142) at
+  // the reference's call sites: the filter of the current minMismatches is built there, and a length
+  // whose filter constructor throws aborts the run (ST_ERROR) at that point and no earlier
+  GWA_HD bool stairOk() {
+    if ((stairBad >> (minMismatches & 63)) & 1) {
+      status = ST_ERROR;
+      return false;
+    }
+    return true;
+  }
+  // getStairCaseMask64bit from the mask words behind the table (offsets outside [-kmax, m]):
+  // offset >= 0: (~0L << (m - offset)) | mask.substring64(offset, offset + 64), else
+  // mask.substring64(0, 64) << -offset (S/StaircaseFilter.java:91-102, A/BitVector.java:106-116)
+  GWA_HD int64_t stairMaskRaw(int kk, int row, int offset) const {
+    const int km = st.kmax, W = (m + 63) / 64;
+    const uint64_t *v = stairTab + (size_t)(km + 2) * (km + 1) * (size_t)(m + km + 1) + (size_t)(kk * (km + 1) + row) * W;
+    auto sub64 = [&](int64_t start, int64_t end) -> int64_t {  // start >= 0
+      const int pos = (int)(start / 64);
+      if (pos >= W) return 0;
+      const int64_t range = end - start, off = start % 64;
+      const int64_t mask = range >= 64 ? ~0LL : ~jshl(~0LL, range);
+      const int64_t low = jushr((int64_t)v[pos], off);
+      const int64_t high = pos + 1 < W ? jshl((int64_t)v[pos + 1] & ~jshl(~0LL, off), 64 - off) : 0LL;
+      return (high | low) & mask;
+    };
+    if (offset >= 0) return jshl(~0LL, m - offset) | sub64(offset, (int64_t)offset + 64);
+    return jshl(sub64(0, 64), -offset);
+  }
   GWA_HD int64_t stairMask(int row, int offset) {
     const int kk = minMismatches;
     if (row >= kk + 1) return 0;
     const int km = st.kmax;
-    if (stairBad) { status = ST_ERROR; return 0; }  // StaircaseFilter ctor throws for this m
+    if ((stairBad >> (kk & 63)) & 1) { status = ST_ERROR; return 0; }  // (never reached: stairOk runs first)
+    if (offset < -km || offset > m) return stairMaskRaw(kk, row, offset);
     const size_t i = (size_t)(kk * (km + 1) + row) * (size_t)(m + km + 1) + (size_t)(offset + km);
     if (stairInLds) return (int64_t)stairLds[i];
     return (int64_t)stairTab[i];
@@ -677,7 +707,7 @@ struct BsfLane {
   }
   GWA_HD static void setCursor(DState<R> &d, int strand, int dir, int start, int end, int cur, int piv) {
     d.flag = (uint8_t)(strand | (dir << 1));
-    d.start = (uint8_t)start; d.end = (uint8_t)end; d.cursor = (uint8_t)cur; d.pivot = (uint8_t)piv;
+    d.start = (uint16_t)start; d.end = (uint16_t)end; d.cursor = (uint16_t)cur; d.pivot = (uint16_t)piv;
   }
 
   // ---- SiSet accessors (A/SiSet.java) ----
@@ -809,17 +839,18 @@ struct BsfLane {
     const int M = cfg.matchScore;
     return M * sumPR - (M + cfg.mismatchPenalty) * (sumK - T) - cfg.splitOpenPenalty * T;
   }
+  // The queue order (SearchState comparator, :141-150: priority ascending, then score() descending,
+  // then processed bases descending) as one unsigned 40-bit key: priority (6 bits; <= k + 1 <= 32) |
+  // 2^23 - 1 - score (24 bits; the host bounds |score| < 2^23 for the batch's scoring and read
+  // lengths, gwa_api.cpp batchTail) | 1023 - processed (10 bits; reads <= 512 bp)
+  GWA_HD static uint64_t packKey(int pr, int sc, int proc) {
+    return ((uint64_t)(pr & 63) << 34) | ((uint64_t)((int64_t)0x7FFFFF - (int64_t)sc) & 0xFFFFFFULL) << 10 |
+           (uint64_t)(1023 - proc);
+  }
   GWA_HD uint64_t keyOf(int s) {
-    if (s == cacheIdx && cache.nextSplit < 0) {
-      const int sc0 = stateScore(cache, 0, false);
-      const uint64_t sp0 = (uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc0) & 0xFFFFFFFFULL;
-      return ((uint64_t)(((uint32_t)cache.state >> 16) & 0xFF) << 40) | (sp0 << 8) | (uint64_t)(255 - cProcessed(cache));
-    }
-    const int sc = chainScore(s, false);
-    const uint64_t sp = (uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc) & 0xFFFFFFFFULL;
-    const int pr = prio(s);
-    const int proc = cProcessed(S(s));
-    return ((uint64_t)pr << 40) | (sp << 8) | (uint64_t)(255 - proc);
+    if (s == cacheIdx && cache.nextSplit < 0)
+      return packKey((int)(((uint32_t)cache.state >> 16) & 0xFF), stateScore(cache, 0, false), cProcessed(cache));
+    return packKey(prio(s), chainScore(s, false), cProcessed(S(s)));
   }
   // Heap slot i: the LDS / slice array of the kernel instance (first tier: LDS), or, with the hybrid
   // heap (HY; k >= 4 kernels: their heaps outgrow a small LDS array, deep heaps are rare), LDS for the
@@ -1874,8 +1905,7 @@ struct BsfLane {
     // keyOf(a) for the chain [a -> b] from the registers (chainScore with one split)
     const int M = cfg.matchScore;
     const int sc = M * (cProcessed(d) + cProcessed(t)) - (M + cfg.mismatchPenalty) * (2 * mk - 1) - cfg.splitOpenPenalty;
-    *key = ((uint64_t)pr << 40) | ((uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc) & 0xFFFFFFFFULL) << 8 |
-           (uint64_t)(255 - cProcessed(d));
+    *key = packKey(pr, sc, cProcessed(d));
     return a;
   }
 
@@ -2049,6 +2079,8 @@ struct BsfLane {
       GWA_PT(te);
       int ch = -1, tt = xT;
       for (; tt < 4 && ch < 0; ++tt) {
+        // StaircaseFilter sf = getStairCaseFilter(m) before the loop over every base (:439)
+        if (tt == 0 && !stairOk()) return SS_DONE;
         const int cand = tt < 0 ? xNextBase : tt;
         if (xCS.state & (1 << cand)) continue;  // isChecked
         xCS.state |= 1 << cand;                 // updateFlag
@@ -2154,6 +2186,8 @@ struct BsfLane {
   }
   // SearchState.nextState (:840-852) from a register copy of the parent, into d; false = null
   GWA_HD bool buildChild(const DState<R> &cs, int ch, DState<R> &d) {
+    // c.nextState(ch, nextSi, queryMask, getStairCaseFilter(m)) (:423-425, :445-447)
+    if (!stairOk()) return false;
     const int strand = cStrand(cs);
     uint64_t rows[R];
     int nh = 0, nko = 0;
@@ -2257,9 +2291,7 @@ struct BsfLane {
     return ok != 0;
   }
   GWA_HD uint64_t keyOfLocal(const DState<R> &c) const {  // keyOf of a chain-free state
-    const int sc = stateScore(c, 0, false);
-    const uint64_t sp = (uint64_t)((int64_t)0x7FFFFFFF - (int64_t)sc) & 0xFFFFFFFFULL;
-    return ((uint64_t)(((uint32_t)c.state >> 16) & 0xFF) << 40) | (sp << 8) | (uint64_t)(255 - cProcessed(c));
+    return packKey((int)(((uint32_t)c.state >> 16) & 0xFF), stateScore(c, 0, false), cProcessed(c));
   }
   GWA_HD int runAhead(int ns) {
 #ifdef GWA_NO_RA
@@ -2331,9 +2363,9 @@ struct BsfLane {
     stairTab = nullptr;
     if (st.base) {
       const uint32_t b = st.base[m];
-      stairBad = b >= 0xFFFFFFFEu;
+      stairBad = b >= 0xFFFFFFFEu ? ~0ULL : st.bad[m];
       stairInLds = (stairLds != nullptr && m == st.ldsM) ? 1 : 0;
-      stairTab = st.tab + (stairBad ? 0 : b);
+      stairTab = st.tab + (b >= 0xFFFFFFFEu ? 0 : b);
     }
     quickSteps = blocks = saReads = maxHeap = kmerLookups = shortSteps = textSteps = textRuns = 0;
     tcW2 = tcWN = -1;

@@ -128,6 +128,7 @@ struct gwa_batch {
   uint32_t *d_count = nullptr;  // [0] search list, [1 + t] overflow list of tier t, [8 + t] tier t work counter
   uint64_t *d_stair = nullptr;
   uint32_t *d_stairBase = nullptr;
+  uint64_t *d_stairBad = nullptr;
   uint32_t hitCap = 4, cigCap = 64;
   uint64_t poolHits = 0, poolCig = 0;  // OutSlots pool behind the fixed slots (grown on demand)
   uint64_t poolUsedH = 0, poolUsedC = 0;
@@ -491,7 +492,7 @@ void gwa_free(void *p) { free(p); }
 
 static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
-                b->d_stair, b->d_stairBase, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
+                b->d_stair, b->d_stairBase, b->d_stairBad, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
                 b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue, b->d_heavy};
   for (void *p : ps)
@@ -567,33 +568,45 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   for (uint32_t m = 0; m < kLenSeen; ++m)
     if (seen[m]) {
       b->maxM = (int)m;
-      if (m <= 255) lens.push_back((int)m);
+      if ((int)m <= kMaxReadLen) lens.push_back((int)m);
     }
-  if (b->maxM > 255)  // the state layout's 8-bit read positions (bsf_core.h); DESIGN.md §1
-    throw std::runtime_error("read longer than 255 bp in this batch (" + std::to_string(b->maxM) +
-                             " bp): the device path aligns reads of at most 255 bp");
+  if (b->maxM > kMaxReadLen)  // 16 query words per strand, 10-bit positions in the queue keys; DESIGN.md §1
+    throw std::runtime_error("read longer than " + std::to_string(kMaxReadLen) + " bp in this batch (" +
+                             std::to_string(b->maxM) + " bp): the device path aligns reads of at most " +
+                             std::to_string(kMaxReadLen) + " bp");
   for (int m : lens) {
     int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
     b->kmax = std::max(b->kmax, k);
   }
   if (b->kmax > 31) throw std::runtime_error("k > 31 is not supported on the device path");
+  {  // the queue keys hold score() in 24 bits (BsfLane::packKey): |score| < 2^23 for these scores
+    const int64_t s = std::max(1, cfg->num_split), T = (s + 1) * s / 2;
+    const int64_t M = std::llabs((int64_t)cfg->match), Nn = std::llabs((int64_t)cfg->mismatch);
+    const int64_t S = std::llabs((int64_t)cfg->split_open);
+    const int64_t bound = M * b->maxM + (M + Nn) * (255 * (s + 1) + T) + S * T;
+    if (cfg->num_split > 64 || bound >= (1LL << 23))
+      throw std::runtime_error("scoring parameters too large for the device's queue keys (|score| may reach " +
+                               std::to_string(bound) + ", limit 2^23)");
+  }
   b->R = b->kmax + 1 <= 4 ? 4 : b->kmax + 1 <= 8 ? 8 : b->kmax + 1 <= 16 ? 16 : 32;
   // report-batch threshold: 14/16 for k <= 3 (C2: 14-16 tie, 12 is 2 % slower; hg19r favours 14),
   // 10/16 for k >= 4 (C4 -m bsf: 8 / 10 / 12 / 14 / 16 -> 447 / 447 / 454 / 489 / 684 ms per 1M reads)
   if (b->scfg.waitQ16 <= 0) b->scfg.waitQ16 = b->R >= 8 ? 10 : 14;
-  std::vector<uint64_t> tab;
+  std::vector<uint64_t> tab, bad;
   std::vector<uint32_t> base;
-  buildStairTables(lens, std::max(b->kmax, 0), tab, base);
+  buildStairTables(lens, std::max(b->kmax, 0), tab, base, bad);
   b->d_stair = devUpload(tab, s, nullptr);
   b->d_stairBase = devUpload(base, s, nullptr);
+  b->d_stairBad = devUpload(bad, s, nullptr);
   b->st.tab = b->d_stair;
   b->st.base = b->d_stairBase;
+  b->st.bad = b->d_stairBad;
   b->st.kmax = std::max(b->kmax, 0);
   b->st.ldsM = -1;
   {  // stage the table of the longest length in LDS when it fits (all reads share it in the usual case)
     const int km = std::max(b->kmax, 0), m0 = b->maxM;
     const uint64_t cnt = (uint64_t)(km + 2) * (km + 1) * (uint64_t)(m0 + km + 1);
-    if (m0 >= 1 && m0 <= 255 && base[(size_t)m0] < 0xFFFFFFFEu && cnt <= (uint64_t)kStairLdsWords) {
+    if (m0 >= 1 && m0 <= kMaxReadLen && base[(size_t)m0] < 0xFFFFFFFEu && cnt <= (uint64_t)kStairLdsWords) {
       b->st.ldsM = m0;
       b->st.ldsBase = base[(size_t)m0];
       b->st.ldsCount = (uint32_t)cnt;
@@ -832,6 +845,9 @@ struct Events {  // destroyed on every path out of gwa_batch_run
 
 static SamText samText(const gwa_batch *b);
 
+// 2-bit query words per strand the kernels keep for reads of up to m bases (QW = 4, 8 or 16)
+static int qwFor(int m) { return m <= 128 ? 4 : m <= 256 ? 8 : 16; }
+
 int gwa_batch_run(gwa_batch_t *b) {
   try {
     gwa_index *ix = b->ix;
@@ -860,7 +876,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     HIPCHK(hipEventRecord(e0, s));
     const bool sf = b->cfg.strategy == 1;
     if (!sf)
-      launchQuickscan(b->maxM <= 128 ? 4 : 8, ix->view, b->scfg, rv, b->d_sres, b->d_oh, outSlots(b), b->d_list[0],
+      launchQuickscan(qwFor(b->maxM), ix->view, b->scfg, rv, b->d_sres, b->d_oh, outSlots(b), b->d_list[0],
                       b->d_count, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
@@ -966,7 +982,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
-      launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+      launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                    ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount,
                    ovfBits, s, (uint32_t *)d_prof, -1);
       {
@@ -986,11 +1002,11 @@ int gwa_batch_run(gwa_batch_t *b) {
       }
 #else
       if (sf)
-        launchSfSearch(b->R, b->maxM <= 128 ? 4 : 8, lanes, ix->view, b->scfg, b->st, rv,
+        launchSfSearch(b->R, qwFor(b->maxM), lanes, ix->view, b->scfg, b->st, rv,
                        (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s);
       else
-        launchSearch(b->R, b->maxM <= 128 ? 4 : 8, deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+        launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                      ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1],
                      ovfCount, ovfBits, s);
 #endif
@@ -1052,7 +1068,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       Caps rc{};
       rc.cigar = 512;
       rc.dpWords = 2 * 4 * (kRescueWindow + 1);  // QW = 8: up to 4 blocks of 64 rows, full history
-      rc.path = 255 + kRescueWindow + 8;
+      rc.path = 256 + kRescueWindow + 8;
       rc.dpSlice = 0;
       const uint64_t stride = laneBytesFor(4, rc);
       uint32_t lanes = std::min<uint32_t>(b->pairs, 65536u);

@@ -14,274 +14,11 @@
 //                   scratch slices and capacity tiers.
 #include <hip/hip_runtime.h>
 
-#include "bsf_core.h"
-#include "sf_core.h"
 #include "sam_core.h"
-#include "kernels.h"
+
+#include "search_kernels.h"
 
 namespace gwa {
-
-__device__ __forceinline__ void waveAppend(bool need, uint32_t value, uint32_t *list, uint32_t *count) {
-  const uint64_t mask = __ballot(need);
-  if (mask == 0) return;
-  const int lane = __lane_id();
-  const int leader = __ffsll((long long)mask) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
-  base = __shfl(base, leader);
-  if (need) {
-    const uint64_t below = lane == 0 ? 0ULL : (mask & ((~0ULL) >> (64 - lane)));
-    list[base + __popcll(below)] = value;
-  }
-}
-
-template <int QW>
-__global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
-                                                           OutHeader *oh, OutSlots os,
-                                                           uint32_t *searchList, uint32_t *searchCount, uint32_t *trace,
-                                                           int traceRead) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  bool need = false;
-  if (r < reads.n) {
-    const uint32_t o = reads.off[r];
-    const int m = (int)reads.len[r];
-    OutHeader *h = oh + r;
-    if (m > 32 * QW || m > 255) {
-      *h = OutHeader{};
-      h->status = ST_TOO_LONG;
-    } else {
-      StairTables st{};
-      LaneMem<4> L{};
-      Caps caps{};
-      BsfLane<4, QW> lane(ix, cfg, st, L, caps);
-      if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
-      lane.initRead(reads.codes + o, m);
-      need = lane.quickPhase(sres + r, h, os, r) != 0;
-      if (lane.trace) trace[0] = (uint32_t)lane.traceN;
-    }
-  }
-  waveAppend(need, r, searchList, searchCount);
-}
-
-#ifndef GWA_SEARCH_WAVES
-#define GWA_SEARCH_WAVES 2
-#endif
-template <int R, int QW, int LH>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES))) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
-                                                         const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
-                                                         uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
-                                                         const int32_t *chrRank,
-                                                         uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
-                                                         uint32_t *ovfBits, uint32_t *trace, int traceRead) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t total = gridDim.x * blockDim.x;
-  // scratch = [lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]
-  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
-  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
-  // first tier: the priority queue lives in LDS, entry i of thread t at heapLds[i * 256 + t]
-  // (heap high-water marks are ~5 entries for k <= 2, 100 bp; larger heaps overflow to tier 1)
-  // LH 2: a sparse deep tier (caps.sparse >= 8, a few long searches, one workgroup per CU): each
-  // active lane holds the top kDeepLdsHeap * sparse / 256 entries of its queue in LDS, contiguous,
-  // and the rest in its slice -- the sift of a queue of thousands of states then waits on HBM for
-  // its lowest levels only
-  __shared__ uint64_t heapLds[LH == 2 ? kDeepLdsHeap : LH ? kLdsHeap * 256 : 1];
-  if (LH == 1) {
-    L.heapP = heapLds + threadIdx.x;
-    L.hs = 256;
-    L.heapL = heapLds + threadIdx.x;  // hybrid heap (k >= 4): LDS for the top slots, the slice beyond
-    L.heapH = kLdsHeap;
-  } else if (LH == 2) {
-    const int per = kDeepLdsHeap / 256 * caps.sparse;
-    L.heapL = heapLds + (threadIdx.x / caps.sparse) * per;
-    L.hsL = 1;
-    L.heapH = per;
-  }
-#ifdef GWA_PROF
-  // profiling build: `trace` is a [lanes][PR_N] cycle-counter array, slot PR_N-1 = wave lifetime
-  uint64_t *prof = (uint64_t *)trace + (size_t)gid * PR_N;
-  const uint64_t tk = clock64();
-  trace = nullptr;
-#endif
-  __shared__ uint64_t stairLds[kStairLdsWords];
-  if (st.ldsM >= 0) {
-    for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
-    __syncthreads();
-  }
-#ifdef GWA_PERREAD_KERNEL
-  {
-    const uint32_t rounds = (n + total - 1) / total;
-    for (uint32_t it = 0; it < rounds; ++it) {
-      const uint32_t i = gid + it * total;
-      bool ovf = false;
-      uint32_t r = 0;
-      if (i < n) {
-        r = list[i];
-        const uint32_t o = reads.off[r];
-        const int m = (int)reads.len[r];
-        BsfLane<R, QW, (LH != 0 && R >= 8)> lane(ix, cfg, st, L, caps);
-        lane.chrRank = chrRank;
-        if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
-        __shared__ uint64_t qwLds1[2 * QW * 256];
-        lane.qwL = (lds_u64 *)(qwLds1 + threadIdx.x);
-        lane.qwS = 256;
-        if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
-        lane.initRead(reads.codes + o, m);
-        lane.searchPhase(sres[r]);
-        lane.writeSearchOutput(oh + r, os, r);
-        if (lane.trace) trace[0] = (uint32_t)lane.traceN;
-        ovf = oh[r].status == ST_OVERFLOW;
-        if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
-      }
-      waveAppend(ovf, r, ovfList, ovfCount);
-    }
-    return;
-  }
-#endif
-  typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8))> Lane;  // hybrid heap: k >= 4 with the LDS heap, sparse tiers
-  Lane lane(ix, cfg, st, L, caps);
-  lane.chrRank = chrRank;
-  if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
-  __shared__ uint64_t qwLds[2 * QW * 256];  // the lanes' 2-bit read words (BsfLane::qword)
-  lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
-  lane.qwS = 256;
-  // the lanes' QueryMask rows (BsfLane::pmL), m <= 128 only (LDS budget: 2 workgroups per CU)
-  __shared__ uint64_t pmLds[QW == 4 ? 2 * 4 * (QW / 2) * 256 : 1];
-  if (QW == 4) {
-    lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
-    lane.pmS = 256;
-  }
-  // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
-  // the wavefront runs the parked reports (DP verification + traceback) together once they are at
-  // least half of its live lanes, instead of once per lane on a divergent path.
-  enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED };
-  int phase = IDLE;
-  uint32_t r = 0;
-  // deep tiers with few reads (caps.sparse > 1): only every caps.sparse-th lane takes reads, so the
-  // long searches of a tier spread over more wavefronts instead of diverging inside few
-  if (caps.sparse > 1 && ((gid & 63) % (uint32_t)caps.sparse) != 0) phase = EXHAUSTED;
-  for (;;) {
-    const bool need = phase == IDLE;
-    const uint64_t needMask = __ballot(need);
-    if (needMask) {
-      const int lid = __lane_id();
-      const int leader = __ffsll((long long)needMask) - 1;
-      uint32_t base = 0;
-      if (lid == leader) base = atomicAdd(work, (uint32_t)__popcll(needMask));
-      base = __shfl(base, leader);
-      if (need) {
-        const uint64_t below = lid == 0 ? 0ULL : (needMask & ((~0ULL) >> (64 - lid)));
-        const uint32_t i = base + (uint32_t)__popcll(below);
-        if (i < n) {
-          r = list[i];
-          const uint32_t o = reads.off[r];
-          const int m = (int)reads.len[r];
-          lane.trace = nullptr;
-          if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; lane.traceN = 0; }
-          lane.initRead(reads.codes + o, m);
-          phase = lane.searchStart(sres[r]) ? RUN : FINISH;
-        } else {
-          phase = EXHAUSTED;
-        }
-      }
-    }
-    if (__ballot(phase != EXHAUSTED) == 0) break;
-    const int nWait = __popcll(__ballot(phase == WAIT));
-    const int nRun = __popcll(__ballot(phase == RUN));
-#ifdef GWA_PROF
-    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_NWAIT] += (uint64_t)nWait;
-#endif
-    if (nWait > 0 && nWait * 16 >= cfg.waitQ16 * (nWait + nRun)) {
-#ifdef GWA_PROF
-      const uint64_t trp = clock64();
-#endif
-      if (phase == WAIT) phase = lane.searchReport() ? RUN : FINISH;
-#ifdef GWA_PROF
-      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_REPORT] += clock64() - trp;
-#endif
-    } else if (phase == RUN) {
-      const int sst = lane.searchStep();
-      phase = sst == Lane::SS_REPORT ? WAIT : sst == Lane::SS_DONE ? FINISH : RUN;
-    }
-    bool ovf = false;
-    if (phase == FINISH) {
-      lane.writeSearchOutput(oh + r, os, r);
-      if (lane.trace) trace[0] = (uint32_t)lane.traceN;
-      ovf = oh[r].status == ST_OVERFLOW;
-      if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
-      phase = IDLE;
-    }
-    waveAppend(ovf, r, ovfList, ovfCount);
-  }
-#ifdef GWA_PROF
-  for (int q = 0; q < PR_N - 1; ++q) prof[q] += lane.prof[q];
-  if (__lane_id() == 0) prof[PR_N - 1] += clock64() - tk;
-#endif
-}
-
-// sf_search<R, QW>: persistent lanes over the read list, one read per lane per iteration (lanes take
-// reads from a shared counter, one atomic per wavefront); overflowing reads go to the next tier.
-template <int R, int QW>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES)))
-sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
-                 uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
-                 const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t total = gridDim.x * blockDim.x;
-  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
-  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
-  __shared__ uint64_t stairLds[kStairLdsWords];
-  if (st.ldsM >= 0) {
-    for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
-    __syncthreads();
-  }
-  __shared__ uint64_t qwLds[2 * QW * 256];
-  SfLane<R, QW> lane(ix, cfg, st, L, caps);
-  lane.chrRank = chrRank;
-  if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
-  lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
-  lane.qwS = 256;
-  __shared__ uint64_t pmLds[QW == 4 ? 2 * 4 * (QW / 2) * 256 : 1];
-  if (QW == 4) {
-    lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
-    lane.pmS = 256;
-  }
-  // the grown last tier (few reads, long searches): every caps.sparse-th lane only, so the searches
-  // run on separate wavefronts instead of serialising inside one (bsf_search_kernel's sparse tiers)
-  if (caps.sparse > 1 && ((gid & 63) % (uint32_t)caps.sparse) != 0) return;
-  for (;;) {
-    const uint64_t act = __ballot(1);
-    const int lid = __lane_id();
-    const int leader = __ffsll((long long)act) - 1;
-    uint32_t base = 0;
-    if (lid == leader) base = atomicAdd(work, (uint32_t)__popcll(act));
-    base = __shfl(base, leader);
-    const uint32_t i = base + (uint32_t)__popcll(act & ((1ULL << lid) - 1ULL));
-    if (i >= n) break;
-    const uint32_t r = list[i];
-    const int m = (int)reads.len[r];
-    OutHeader *h = oh + r;
-    bool ovf = false;
-    if (m > 32 * QW || m > 255) {
-      OutHeader z{};
-      z.status = ST_TOO_LONG;
-      *h = z;
-    } else {
-      lane.initRead(reads.codes + reads.off[r], m);
-      lane.sfSearch();
-      lane.writeSearchOutput(h, os, r);
-      h->states = lane.created;  // (nStates is the arena's high-water mark: slots are recycled)
-      h->quickSteps = lane.quickSteps;
-      h->blocks = 0;  // (all Occ blocks are in searchBlocks on this path)
-      h->kmerLookups = lane.kmerLookups;
-      h->quickShort = lane.shortSteps;
-      h->quickSa = 0;
-      h->quickText = 0;
-      ovf = h->status == ST_OVERFLOW;
-      if (ovf) atomicOr(ovfBits, (uint32_t)h->ovfWhat);
-    }
-    waveAppend(ovf, r, ovfList, ovfCount);
-  }
-}
 
 // Paired-end pair choice and mate rescue (orc_align_pairs rules 1-3, oracle/gwa_oracle.cpp
 // orc_align_pairs / peRescue; the build's own design -- the reference has no paired-end path).
@@ -325,9 +62,9 @@ __global__ void __launch_bounds__(64) pair_rescue_kernel(IndexView ix, SearchCon
           lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
           lane.qwS = 64;
           lane.initRead(reads.codes + reads.off[r], m);
-          const int countN = m > 0 && m <= 255 ? lane.buildMasks() : 0x7FFF;
+          const int countN = m > 0 && m <= 256 ? lane.buildMasks() : 0x7FFF;
           const int k = lane.k;
-          if (m > 0 && m <= 255 && k >= 0 && countN <= k) {
+          if (m > 0 && m <= 256 && k >= 0 && countN <= k) {  // (QW = 8: mates up to 256 bp are rescued)
             const int kr = k > m / 10 ? k : m / 10;
             const int64_t off = ix.contigOff[an.chr];
             const int64_t clen = (an.chr + 1 < ix.nContig ? ix.contigOff[an.chr + 1] : (int64_t)ix.N) - off;
@@ -556,13 +293,9 @@ void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const
                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace, int traceRead) {
   if (reads.n == 0) return;
-  dim3 grid((reads.n + 255) / 256);
-  if (QW == 4)
-    hipLaunchKernelGGL(fm_quickscan_kernel<4>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
-                       searchList, searchCount, trace, traceRead);
-  else
-    hipLaunchKernelGGL(fm_quickscan_kernel<8>, grid, dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
-                       searchList, searchCount, trace, traceRead);
+  if (QW == 4) launchQuickscanT<4>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
+  else if (QW == 8) launchQuickscanT<8>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
+  else launchQuickscan16(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
 }
 
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,
@@ -571,28 +304,15 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
                   const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
                   hipStream_t s, uint32_t *trace, int traceRead) {
   if (n == 0) return;
-  dim3 grid((lanes + 255) / 256);
-  const int key = (R * 16 + QW) * 3 + (ldsHeap == 2 ? 2 : ldsHeap ? 1 : 0);
-  switch (key) {
-#define GWA_CASE(RR, QQ, LL)                                                                                          \
-  case (RR * 16 + QQ) * 3 + LL:                                                                                       \
-    hipLaunchKernelGGL((bsf_search_kernel<RR, QQ, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
-                       scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits,                 \
-                       trace, traceRead);                                                                             \
-    break;
-#define GWA_CASE2(RR, QQ) GWA_CASE(RR, QQ, 0) GWA_CASE(RR, QQ, 1) GWA_CASE(RR, QQ, 2)
-    GWA_CASE2(4, 4)
-    GWA_CASE2(4, 8)
-    GWA_CASE2(8, 4)
-    GWA_CASE2(8, 8)
-    GWA_CASE2(16, 4)
-    GWA_CASE2(16, 8)
-    GWA_CASE2(32, 4)
-    GWA_CASE2(32, 8)
-#undef GWA_CASE2
-#undef GWA_CASE
-    default: break;
-  }
+  if (QW == 4)
+    launchSearchT<4>(R, ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, work,
+                     ovfList, ovfCount, ovfBits, s, trace, traceRead);
+  else if (QW == 8)
+    launchSearchT<8>(R, ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, work,
+                     ovfList, ovfCount, ovfBits, s, trace, traceRead);
+  else
+    launchSearch16(R, ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, work,
+                   ovfList, ovfCount, ovfBits, s, trace, traceRead);
 }
 
 void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
@@ -601,24 +321,15 @@ void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const Se
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
                     hipStream_t s) {
   if (n == 0) return;
-  dim3 grid((lanes + 255) / 256);
-  switch (R * 16 + QW) {
-#define GWA_SF(RR, QQ)                                                                                               \
-  case RR * 16 + QQ:                                                                                                 \
-    hipLaunchKernelGGL((sf_search_kernel<RR, QQ>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,      \
-                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);                         \
-    break;
-    GWA_SF(4, 4)
-    GWA_SF(4, 8)
-    GWA_SF(8, 4)
-    GWA_SF(8, 8)
-    GWA_SF(16, 4)
-    GWA_SF(16, 8)
-    GWA_SF(32, 4)
-    GWA_SF(32, 8)
-#undef GWA_SF
-    default: break;
-  }
+  if (QW == 4)
+    launchSfSearchT<4>(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
+                       ovfCount, ovfBits, s);
+  else if (QW == 8)
+    launchSfSearchT<8>(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
+                       ovfCount, ovfBits, s);
+  else
+    launchSfSearch16(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
+                     ovfCount, ovfBits, s);
 }
 
 size_t laneBytesFor(int R, const Caps &c) {

@@ -98,12 +98,16 @@ struct ReadsView {
 // row in [0, kmax], offset in [-kmax, m]:  tab[base(m) + ((kk*(kmax+1) + row)*(m+kmax+1) + offset+kmax)]
 struct StairTables {
   const uint64_t *tab;
-  const uint32_t *base;  // per m (0..255), index into tab; 0xFFFFFFFF = no table
+  const uint32_t *base;  // per m (0..kMaxReadLen), index into tab; 0xFFFFFFFF = no table
   int32_t kmax;
   int32_t ldsM;          // reads of this length use a copy of their table staged in LDS (-1 = none)
   uint32_t ldsBase, ldsCount;  // that table: tab[ldsBase, ldsBase + ldsCount)
+  const uint64_t *bad;   // per m: bit kk set when StaircaseFilter(m, kk) throws (S/StaircaseFilter.java:47-72)
 };
 constexpr int kStairLdsWords = 2048;  // 16 KiB of LDS per workgroup
+// Longest read of the device path: 16 two-bit query words per strand (QW = 16), 10-bit read positions
+// in the queue key (BsfLane::packKey), 16-bit cursor fields (DState)
+constexpr int kMaxReadLen = 512;
 constexpr int kLdsHeap = 8;           // first-tier priority-queue capacity (entries, in LDS)
 constexpr int kDeepLdsHeap = 8192;    // LDS queue entries per workgroup of a sparse deep tier (64 KiB)
 

@@ -217,15 +217,18 @@ struct BV {
 inline int8_t jb(int x) { return (int8_t)(uint8_t)(uint32_t)x; }
 }  // namespace
 
-void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uint64_t> &tab, std::vector<uint32_t> &base) {
-  base.assign(256, 0xFFFFFFFFu);
+void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uint64_t> &tab, std::vector<uint32_t> &base,
+                      std::vector<uint64_t> &bad) {
+  base.assign(kMaxReadLen + 1, 0xFFFFFFFFu);
+  bad.assign(kMaxReadLen + 1, 0);
   tab.clear();
   for (int m : lengths) {
-    if (m < 0 || m > 255 || base[(size_t)m] != 0xFFFFFFFFu) continue;
+    if (m < 0 || m > kMaxReadLen || base[(size_t)m] != 0xFFFFFFFFu) continue;
     const size_t perRow = (size_t)(m + kmax + 1);
     const size_t start = tab.size();
-    tab.resize(start + (size_t)(kmax + 2) * (size_t)(kmax + 1) * perRow, 0);
-    bool threw = false;
+    const size_t W = (size_t)(m + 63) / 64, rawAt = start + (size_t)(kmax + 2) * (size_t)(kmax + 1) * perRow;
+    tab.resize(rawAt + (size_t)(kmax + 2) * (size_t)(kmax + 1) * W, 0);
+    uint64_t threw = 0;  // bit kk: StaircaseFilter(m, kk) throws
     for (int kk = 0; kk <= kmax + 1; ++kk) {
       try {
         int lastChunkSize = (m - kk >= 6) ? m * 2 / (kk + 2) : m - kk;
@@ -249,11 +252,16 @@ void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uin
             else val = jl(masks[(size_t)row].sub64(0, 64), -off);
             tab[start + ((size_t)kk * (size_t)(kmax + 1) + (size_t)row) * perRow + (size_t)(off + kmax)] = (uint64_t)val;
           }
+        // the masks themselves, for offsets outside [-kmax, m] (BsfLane::stairMask)
+        for (int row = 0; row < (int)masks.size() && row <= kmax; ++row)
+          for (size_t w = 0; w < W && w < masks[(size_t)row].b.size(); ++w)
+            tab[rawAt + ((size_t)kk * (size_t)(kmax + 1) + (size_t)row) * W + w] = (uint64_t)masks[(size_t)row].b[w];
       } catch (JavaThrow &) {
-        threw = true;
+        threw |= 1ULL << kk;
       }
     }
-    base[(size_t)m] = threw ? 0xFFFFFFFEu : (uint32_t)start;
+    base[(size_t)m] = (uint32_t)start;
+    bad[(size_t)m] = threw;
   }
   if (tab.empty()) tab.push_back(0);
 }

@@ -32,7 +32,12 @@ bool cyclicSAHost(const uint8_t *codes, uint64_t n, std::vector<uint32_t> &sa, i
 // Derive BWT Occ blocks, 2-bit text, C[] from T and the two SAs.
 void finishIndex(HostIndex &ix);
 // Staircase tables for read lengths in `lengths` and k up to kmax.
-void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uint64_t> &tab, std::vector<uint32_t> &base);
+// per read length m <= kMaxReadLen: the tables of every kk in [0, kmax + 1] (base[m]) and the kk whose
+// StaircaseFilter(m, kk) constructor throws in the reference (bit kk of bad[m]; its table is zeros).
+// Behind each length's table: the staircase masks themselves, ceil(m / 64) words per (kk, row)
+// (offsets outside [-kmax, m], which only chunks with wrapped (byte) starts reach)
+void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uint64_t> &tab, std::vector<uint32_t> &base,
+                      std::vector<uint64_t> &bad);
 
 // Java-String.compareTo-consistent ranks of contig names
 void rankNames(HostIndex &ix);

@@ -1,0 +1,345 @@
+// search_kernels.h -- the per-read search kernels of the align path (gwa_kernels.hip), as templates
+// instantiated by gwa_kernels.hip (query words QW = 4, 8: reads <= 256 bp) and gwa_kernels_long.hip
+// (QW = 16: reads <= 512 bp), so the long-read instances compile in their own translation unit.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "bsf_core.h"
+#include "sf_core.h"
+#include "kernels.h"
+
+namespace gwa {
+
+
+__device__ __forceinline__ void waveAppend(bool need, uint32_t value, uint32_t *list, uint32_t *count) {
+  const uint64_t mask = __ballot(need);
+  if (mask == 0) return;
+  const int lane = __lane_id();
+  const int leader = __ffsll((long long)mask) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader);
+  if (need) {
+    const uint64_t below = lane == 0 ? 0ULL : (mask & ((~0ULL) >> (64 - lane)));
+    list[base + __popcll(below)] = value;
+  }
+}
+
+template <int QW>
+__global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
+                                                           OutHeader *oh, OutSlots os,
+                                                           uint32_t *searchList, uint32_t *searchCount, uint32_t *trace,
+                                                           int traceRead) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  bool need = false;
+  if (r < reads.n) {
+    const uint32_t o = reads.off[r];
+    const int m = (int)reads.len[r];
+    OutHeader *h = oh + r;
+    if (m > 32 * QW) {
+      *h = OutHeader{};
+      h->status = ST_TOO_LONG;
+    } else {
+      StairTables st{};
+      LaneMem<4> L{};
+      Caps caps{};
+      BsfLane<4, QW> lane(ix, cfg, st, L, caps);
+      if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
+      lane.initRead(reads.codes + o, m);
+      need = lane.quickPhase(sres + r, h, os, r) != 0;
+      if (lane.trace) trace[0] = (uint32_t)lane.traceN;
+    }
+  }
+  waveAppend(need, r, searchList, searchCount);
+}
+
+#ifndef GWA_SEARCH_WAVES
+#define GWA_SEARCH_WAVES 2
+#endif
+template <int R, int QW, int LH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES))) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
+                                                         const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
+                                                         uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
+                                                         const int32_t *chrRank,
+                                                         uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
+                                                         uint32_t *ovfBits, uint32_t *trace, int traceRead) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = gridDim.x * blockDim.x;
+  // scratch = [lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]
+  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
+  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+  // first tier: the priority queue lives in LDS, entry i of thread t at heapLds[i * 256 + t]
+  // (heap high-water marks are ~5 entries for k <= 2, 100 bp; larger heaps overflow to tier 1)
+  // LH 2: a sparse deep tier (caps.sparse >= 8, a few long searches, one workgroup per CU): each
+  // active lane holds the top kDeepLdsHeap * sparse / 256 entries of its queue in LDS, contiguous,
+  // and the rest in its slice -- the sift of a queue of thousands of states then waits on HBM for
+  // its lowest levels only
+  __shared__ uint64_t heapLds[LH == 2 ? kDeepLdsHeap : LH ? kLdsHeap * 256 : 1];
+  if (LH == 1) {
+    L.heapP = heapLds + threadIdx.x;
+    L.hs = 256;
+    L.heapL = heapLds + threadIdx.x;  // hybrid heap (k >= 4): LDS for the top slots, the slice beyond
+    L.heapH = kLdsHeap;
+  } else if (LH == 2) {
+    const int per = kDeepLdsHeap / 256 * caps.sparse;
+    L.heapL = heapLds + (threadIdx.x / caps.sparse) * per;
+    L.hsL = 1;
+    L.heapH = per;
+  }
+#ifdef GWA_PROF
+  // profiling build: `trace` is a [lanes][PR_N] cycle-counter array, slot PR_N-1 = wave lifetime
+  uint64_t *prof = (uint64_t *)trace + (size_t)gid * PR_N;
+  const uint64_t tk = clock64();
+  trace = nullptr;
+#endif
+  __shared__ uint64_t stairLds[kStairLdsWords];
+  if (st.ldsM >= 0) {
+    for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
+    __syncthreads();
+  }
+#ifdef GWA_PERREAD_KERNEL
+  {
+    const uint32_t rounds = (n + total - 1) / total;
+    for (uint32_t it = 0; it < rounds; ++it) {
+      const uint32_t i = gid + it * total;
+      bool ovf = false;
+      uint32_t r = 0;
+      if (i < n) {
+        r = list[i];
+        const uint32_t o = reads.off[r];
+        const int m = (int)reads.len[r];
+        BsfLane<R, QW, (LH != 0 && R >= 8)> lane(ix, cfg, st, L, caps);
+        lane.chrRank = chrRank;
+        if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
+        __shared__ uint64_t qwLds1[2 * QW * 256];
+        lane.qwL = (lds_u64 *)(qwLds1 + threadIdx.x);
+        lane.qwS = 256;
+        if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
+        lane.initRead(reads.codes + o, m);
+        lane.searchPhase(sres[r]);
+        lane.writeSearchOutput(oh + r, os, r);
+        if (lane.trace) trace[0] = (uint32_t)lane.traceN;
+        ovf = oh[r].status == ST_OVERFLOW;
+        if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
+      }
+      waveAppend(ovf, r, ovfList, ovfCount);
+    }
+    return;
+  }
+#endif
+  typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8))> Lane;  // hybrid heap: k >= 4 with the LDS heap, sparse tiers
+  Lane lane(ix, cfg, st, L, caps);
+  lane.chrRank = chrRank;
+  if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
+  __shared__ uint64_t qwLds[2 * QW * 256];  // the lanes' 2-bit read words (BsfLane::qword)
+  lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
+  lane.qwS = 256;
+  // the lanes' QueryMask rows (BsfLane::pmL), m <= 128 only (LDS budget: 2 workgroups per CU)
+  __shared__ uint64_t pmLds[QW == 4 ? 2 * 4 * (QW / 2) * 256 : 1];
+  if (QW == 4) {
+    lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
+    lane.pmS = 256;
+  }
+  // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
+  // the wavefront runs the parked reports (DP verification + traceback) together once they are at
+  // least half of its live lanes, instead of once per lane on a divergent path.
+  enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED };
+  int phase = IDLE;
+  uint32_t r = 0;
+  // deep tiers with few reads (caps.sparse > 1): only every caps.sparse-th lane takes reads, so the
+  // long searches of a tier spread over more wavefronts instead of diverging inside few
+  if (caps.sparse > 1 && ((gid & 63) % (uint32_t)caps.sparse) != 0) phase = EXHAUSTED;
+  for (;;) {
+    const bool need = phase == IDLE;
+    const uint64_t needMask = __ballot(need);
+    if (needMask) {
+      const int lid = __lane_id();
+      const int leader = __ffsll((long long)needMask) - 1;
+      uint32_t base = 0;
+      if (lid == leader) base = atomicAdd(work, (uint32_t)__popcll(needMask));
+      base = __shfl(base, leader);
+      if (need) {
+        const uint64_t below = lid == 0 ? 0ULL : (needMask & ((~0ULL) >> (64 - lid)));
+        const uint32_t i = base + (uint32_t)__popcll(below);
+        if (i < n) {
+          r = list[i];
+          const uint32_t o = reads.off[r];
+          const int m = (int)reads.len[r];
+          lane.trace = nullptr;
+          if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; lane.traceN = 0; }
+          lane.initRead(reads.codes + o, m);
+          phase = lane.searchStart(sres[r]) ? RUN : FINISH;
+        } else {
+          phase = EXHAUSTED;
+        }
+      }
+    }
+    if (__ballot(phase != EXHAUSTED) == 0) break;
+    const int nWait = __popcll(__ballot(phase == WAIT));
+    const int nRun = __popcll(__ballot(phase == RUN));
+#ifdef GWA_PROF
+    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_NWAIT] += (uint64_t)nWait;
+#endif
+    if (nWait > 0 && nWait * 16 >= cfg.waitQ16 * (nWait + nRun)) {
+#ifdef GWA_PROF
+      const uint64_t trp = clock64();
+#endif
+      if (phase == WAIT) phase = lane.searchReport() ? RUN : FINISH;
+#ifdef GWA_PROF
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_REPORT] += clock64() - trp;
+#endif
+    } else if (phase == RUN) {
+      const int sst = lane.searchStep();
+      phase = sst == Lane::SS_REPORT ? WAIT : sst == Lane::SS_DONE ? FINISH : RUN;
+    }
+    bool ovf = false;
+    if (phase == FINISH) {
+      lane.writeSearchOutput(oh + r, os, r);
+      if (lane.trace) trace[0] = (uint32_t)lane.traceN;
+      ovf = oh[r].status == ST_OVERFLOW;
+      if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
+      phase = IDLE;
+    }
+    waveAppend(ovf, r, ovfList, ovfCount);
+  }
+#ifdef GWA_PROF
+  for (int q = 0; q < PR_N - 1; ++q) prof[q] += lane.prof[q];
+  if (__lane_id() == 0) prof[PR_N - 1] += clock64() - tk;
+#endif
+}
+
+// sf_search<R, QW>: persistent lanes over the read list, one read per lane per iteration (lanes take
+// reads from a shared counter, one atomic per wavefront); overflowing reads go to the next tier.
+template <int R, int QW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES)))
+sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
+                 uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
+                 const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = gridDim.x * blockDim.x;
+  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
+  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+  __shared__ uint64_t stairLds[kStairLdsWords];
+  if (st.ldsM >= 0) {
+    for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
+    __syncthreads();
+  }
+  __shared__ uint64_t qwLds[2 * QW * 256];
+  SfLane<R, QW> lane(ix, cfg, st, L, caps);
+  lane.chrRank = chrRank;
+  if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
+  lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
+  lane.qwS = 256;
+  __shared__ uint64_t pmLds[QW == 4 ? 2 * 4 * (QW / 2) * 256 : 1];
+  if (QW == 4) {
+    lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
+    lane.pmS = 256;
+  }
+  // the grown last tier (few reads, long searches): every caps.sparse-th lane only, so the searches
+  // run on separate wavefronts instead of serialising inside one (bsf_search_kernel's sparse tiers)
+  if (caps.sparse > 1 && ((gid & 63) % (uint32_t)caps.sparse) != 0) return;
+  for (;;) {
+    const uint64_t act = __ballot(1);
+    const int lid = __lane_id();
+    const int leader = __ffsll((long long)act) - 1;
+    uint32_t base = 0;
+    if (lid == leader) base = atomicAdd(work, (uint32_t)__popcll(act));
+    base = __shfl(base, leader);
+    const uint32_t i = base + (uint32_t)__popcll(act & ((1ULL << lid) - 1ULL));
+    if (i >= n) break;
+    const uint32_t r = list[i];
+    const int m = (int)reads.len[r];
+    OutHeader *h = oh + r;
+    bool ovf = false;
+    if (m > 32 * QW) {
+      OutHeader z{};
+      z.status = ST_TOO_LONG;
+      *h = z;
+    } else {
+      lane.initRead(reads.codes + reads.off[r], m);
+      lane.sfSearch();
+      lane.writeSearchOutput(h, os, r);
+      h->states = lane.created;  // (nStates is the arena's high-water mark: slots are recycled)
+      h->quickSteps = lane.quickSteps;
+      h->blocks = 0;  // (all Occ blocks are in searchBlocks on this path)
+      h->kmerLookups = lane.kmerLookups;
+      h->quickShort = lane.shortSteps;
+      h->quickSa = 0;
+      h->quickText = 0;
+      ovf = h->status == ST_OVERFLOW;
+      if (ovf) atomicOr(ovfBits, (uint32_t)h->ovfWhat);
+    }
+    waveAppend(ovf, r, ovfList, ovfCount);
+  }
+}
+
+
+template <int QW>
+void launchQuickscanT(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
+                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
+                      int traceRead) {
+  hipLaunchKernelGGL(fm_quickscan_kernel<QW>, dim3((reads.n + 255) / 256), dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
+                     searchList, searchCount, trace, traceRead);
+}
+
+template <int QW>
+void launchSearchT(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
+                   uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank,
+                   uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s,
+                   uint32_t *trace, int traceRead) {
+  dim3 grid((lanes + 255) / 256);
+  const int key = R * 3 + (ldsHeap == 2 ? 2 : ldsHeap ? 1 : 0);
+  switch (key) {
+#define GWA_CASE(RR, LL)                                                                                               \
+  case RR * 3 + LL:                                                                                                    \
+    hipLaunchKernelGGL((bsf_search_kernel<RR, QW, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,      \
+                       scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, trace, traceRead); \
+    break;
+#define GWA_CASE2(RR) GWA_CASE(RR, 0) GWA_CASE(RR, 1) GWA_CASE(RR, 2)
+    GWA_CASE2(4)
+    GWA_CASE2(8)
+    GWA_CASE2(16)
+    GWA_CASE2(32)
+#undef GWA_CASE2
+#undef GWA_CASE
+    default: break;
+  }
+}
+
+template <int QW>
+void launchSfSearchT(int R, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
+                     const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
+                     uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s) {
+  dim3 grid((lanes + 255) / 256);
+  switch (R) {
+#define GWA_SF(RR)                                                                                                     \
+  case RR:                                                                                                             \
+    hipLaunchKernelGGL((sf_search_kernel<RR, QW>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,        \
+                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);                           \
+    break;
+    GWA_SF(4)
+    GWA_SF(8)
+    GWA_SF(16)
+    GWA_SF(32)
+#undef GWA_SF
+    default: break;
+  }
+}
+
+// the QW = 16 instances (gwa_kernels_long.hip)
+void launchQuickscan16(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
+                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
+                       int traceRead);
+void launchSearch16(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                    const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
+                    uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank,
+                    uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s,
+                    uint32_t *trace, int traceRead);
+void launchSfSearch16(int R, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                      const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
+                      const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
+                      uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s);
+
+}  // namespace gwa

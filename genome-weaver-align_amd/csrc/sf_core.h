@@ -20,8 +20,9 @@ template <int R>
 struct SfState {
   uint32_t lb, ub;
   int32_t score;
-  uint8_t strand, offset, index, nrows;
-  uint8_t kOffset, hasHit, meta, pad;
+  int16_t offset, index;  // read positions (reads up to 512 bp; negative after a wrapped (byte) chunk start)
+  uint8_t strand, nrows, kOffset, hasHit;
+  uint8_t meta, pad[3];
   uint64_t nfa[R];
 };
 static_assert(sizeof(SfState<4>) <= sizeof(DState<4>), "SfState must fit the DState arena slots");
@@ -120,8 +121,8 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     ++created;
     SfState<R> d;
     d.lb = lb; d.ub = ub; d.score = score;
-    d.strand = (uint8_t)strand; d.offset = (uint8_t)offset; d.index = (uint8_t)index; d.nrows = (uint8_t)nrows;
-    d.kOffset = (uint8_t)kOffset; d.hasHit = hasHit ? 1 : 0; d.meta = meta; d.pad = 0;
+    d.strand = (uint8_t)strand; d.offset = (int16_t)offset; d.index = (int16_t)index; d.nrows = (uint8_t)nrows;
+    d.kOffset = (uint8_t)kOffset; d.hasHit = hasHit ? 1 : 0; d.meta = meta;
 #pragma unroll
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nrows ? rows[i] : 0ULL;
     arena()[id] = d;
@@ -207,10 +208,7 @@ struct SfLane : BsfLane<R, QW, false, 24> {
   GWA_HD bool sfStart() {
     const int countN = B::buildMasks();
     if (countN > k) return false;  // reported unmapped (:232-236)
-    if (B::stairBad) {             // StaircaseFilter(m, k + 1) throws (getStairCaseFilter, :140-142)
-      status = ST_ERROR;
-      return false;
-    }
+    if (!B::stairOk()) return false;  // StaircaseFilter(m, k + 1) throws (PrefixScan.scanRead's filter, :244)
     const int kk = minMismatches;  // k + 1
     const int nch = kk + 1;
     const int mCap = (m + 63) / 64 * 64;  // ACGTSequence storage: positions past it throw
@@ -221,12 +219,20 @@ struct SfLane : BsfLane<R, QW, false, 24> {
       for (int c = 0; c < nch; ++c) {
         int cs = 0, w = 0;
         chunk(m, kk, c, &cs, &w);
-        if (cs < 0 || cs + (w > 0 ? w : 0) > mCap) {  // ArrayIndexOutOfBounds in getACGT
+        // getACGT outside the read's storage throws ArrayIndexOutOfBounds when the scan reaches it:
+        // at once below 0, at mCap unless a mismatch ends the chunk first.  A chunk of width <= 0
+        // (the reference's (byte) chunk starts wrap for long reads) scans nothing.
+        if (w > 0 && cs < 0) {
           status = ST_ERROR;
           return false;
         }
+        const bool past = w > 0 && cs + w > mCap;
         uint32_t lb = 0, ub = (uint32_t)ix.N;  // an empty chunk keeps wholeSARange
-        const int r = w > 0 ? scanChunk(strand, cs, w, &lb, &ub) : 1;
+        const int r = w > 0 ? scanChunk(strand, cs, past ? mCap - cs : w, &lb, &ub) : 1;
+        if (past && r != 0) {
+          status = ST_ERROR;
+          return false;
+        }
         if (r == 0) continue;  // chunkWithMismatch
         const int score = cfg.matchScore * w;
         const int id = newState(strand, cs, cs + w, score, lb, ub, r == 2 ? M_TEXT : 0, init, k + 1, 0, false);
@@ -306,6 +312,7 @@ struct SfLane : BsfLane<R, QW, false, 24> {
   // SFState.nextState (:448-460) + ReadAlignmentNFA.nextState(nextACGTIndex, progress, m, ...)
   // (S/ReadAlignmentNFA.java:136-144); pushes the child; false = the search ends
   GWA_HD bool child(const SfState<R> &c, int ch, uint32_t lb, uint32_t ub) {
+    if (!B::stairOk()) return false;  // c.nextState(..., getStairCaseFilter(m)) (:282)
     const int nextIndex = c.index + 1;
     const int kr = c.nrows - 1;
     const int64_t qeq = B::patternMask64(c.strand, true, nextIndex, 0, nextIndex, ch, kr);

@@ -60,10 +60,21 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
     OutHeader hd{};
     std::vector<uint32_t> tv(65537, 0);
     bool traced = false;
-    for (int t = 0; t < 4; ++t) {
+    // tiers 0-3, then the last tier with every capacity doubled per rerun (gwa_batch_run grows the
+    // exceeded ones; doubling all of them gives the same results, capacities only decide overflow)
+    for (int t = 0; t < 14; ++t) {
+      Caps sc = sfTiers[t < 4 ? t : 3], bc = tiers[t < 4 ? t : 3];
+      if (t >= 4) {
+        const int g = t - 3;
+        for (Caps *c : {&sc, &bc}) {
+          c->arena <<= g; c->heap <<= g; c->hits <<= g; c->list <<= g; c->cigar <<= g; c->cand <<= g;
+        }
+        const size_t need = std::max(laneBytes<R>(sc), laneBytes<R>(bc)) + ilvBytes(bc) + 4096;
+        if (scratch.size() < need) scratch.resize(need);
+      }
       if (strategy == 1) {
-        LaneMem<R> L = laneMem<R>(scratch.data(), sfTiers[t]);
-        SfLane<R, QW> lane(x->v, cfg, st, L, sfTiers[t]);
+        LaneMem<R> L = laneMem<R>(scratch.data(), sc);
+        SfLane<R, QW> lane(x->v, cfg, st, L, sc);
         lane.chrRank = rk.data();
         lane.initRead(codes.data(), (int)mlen);
         hd = OutHeader{};
@@ -74,8 +85,8 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         if (hd.status != ST_OVERFLOW) break;
         continue;
       }
-      LaneMem<R> L = laneMem<R>(scratch.data(), tiers[t]);
-      BsfLane<R, QW> lane(x->v, cfg, st, L, tiers[t]);
+      LaneMem<R> L = laneMem<R>(scratch.data(), bc);
+      BsfLane<R, QW> lane(x->v, cfg, st, L, bc);
       lane.chrRank = rk.data();
       const char *tre = getenv("GWA_TRACE_READ");
       const char *qtre = getenv("GWA_QTRACE_READ");
@@ -186,21 +197,25 @@ int hc_align(void *p, float k, int reportType, int numSplit, int strategy, uint3
     int kk = (k > 0 && k < 1) ? (int)floor((double)((float)m * k)) : (int)k;
     kmax = std::max(kmax, kk);
   }
-  std::vector<uint64_t> tab;
+  std::vector<uint64_t> tab, bad;
   std::vector<uint32_t> base;
-  buildStairTables(lens, kmax, tab, base);
-  StairTables st{tab.data(), base.data(), kmax, -1, 0, 0};
+  buildStairTables(lens, kmax, tab, base, bad);
+  StairTables st{tab.data(), base.data(), kmax, -1, 0, 0, bad.data()};
   std::string sam;
   int maxM = 1;
   for (int m : lens) maxM = std::max(maxM, m);
   int R = kmax + 1 <= 4 ? 4 : kmax + 1 <= 8 ? 8 : kmax + 1 <= 16 ? 16 : 32;
   int rc = 0;
+  if (maxM > kMaxReadLen) return -9;
+  // QW as gwa_api.cpp qwFor
+#define HC_RUN(RR) (maxM <= 128 ? runAll<RR, 4> : maxM <= 256 ? runAll<RR, 8> : runAll<RR, 16>)
   switch (R) {
-    case 4: rc = (maxM <= 128 ? runAll<4, 4> : runAll<4, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    case 8: rc = (maxM <= 128 ? runAll<8, 4> : runAll<8, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    case 16: rc = (maxM <= 128 ? runAll<16, 4> : runAll<16, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
-    default: rc = (maxM <= 128 ? runAll<32, 4> : runAll<32, 8>)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 4: rc = HC_RUN(4)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 8: rc = HC_RUN(8)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    case 16: rc = HC_RUN(16)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
+    default: rc = HC_RUN(32)(x, strategy, cfg, st, maxM, kmax, n, names, seqs, quals, sam, stats); break;
   }
+#undef HC_RUN
   if (rc != 0) return rc;
   *out = (char *)malloc(sam.size() + 1);
   memcpy(*out, sam.c_str(), sam.size() + 1);

@@ -142,24 +142,50 @@ def test_edge_reads(random_pair):
     _check(gi, oi, [(a, b, None) for a, b, c in reads], k=2.0)
 
 
-def test_reads_longer_than_255_fail_at_batch_creation(random_pair, gwa):
-    """The device path aligns reads of at most 255 bp: a longer read fails the
-    batch before any kernel runs, with the limit in the message.  200 bp reads align as the oracle
-    does; at 224-255 bp the reference algorithm itself throws (BitVector._lshift out of bounds, the
-    oracle reproduces it) and the device path aborts the batch the same way."""
+from test_hostcore import LONG_CASES  # noqa: E402
+
+
+@pytest.mark.parametrize("strategy,m,k", LONG_CASES)
+def test_long_reads_on_gpu(random_pair, gwa, strategy, m, k):
+    """Reads of 257..512 bp (QW = 16 kernels).  Above ~223 bp the reference's StaircaseFilter (byte)
+    chunk starts wrap and some reads make it throw: the reads the oracle aligns give its SAM as one
+    batch; a batch holding a read the oracle throws on fails as the reference's run aborts; a read
+    over 512 bp fails the batch at creation, with the limit in the message."""
     codes, names, lengths, gi, oi = random_pair
-    seqs, rn = synth.reads(codes, lengths, 40, 200, 2, config_id=7)
+    seqs, rn = synth.reads(codes, lengths, 60, m, 3, config_id=4 + m)
     strs = synth.to_strings(seqs)
-    _check(gi, oi, [(rn[i], strs[i], None) for i in range(len(strs))], k=2.0)
-    seqs, rn = synth.reads(codes, lengths, 20, 255, 2, config_id=7)
-    strs = synth.to_strings(seqs)
-    reads = [(rn[i], strs[i], None) for i in range(len(strs))]
-    with pytest.raises(RuntimeError, match="ArrayIndexOutOfBounds"):
-        oi.align(reads, O.OrcConfig.default(k=2.0))
-    with pytest.raises(gwa.GwaError, match="reference would abort"):
-        gwa.BidirectionalSuffixFilter(gi).align_batch(reads)
-    with pytest.raises(gwa.GwaError, match="255"):
-        gwa.BidirectionalSuffixFilter(gi).align_batch([("ok", strs[0][:100], None), ("long", strs[1] + "A", None)])
+    strat = ["bsf", "sf"][strategy]
+    good, bad = [], []
+    for i, s_ in enumerate(strs):
+        r = ("r%d" % i, s_, "I" * m)
+        try:
+            oi.align([r], O.OrcConfig.default(k=k, strategy=strategy))
+            good.append(r)
+        except RuntimeError:
+            bad.append(r)
+    assert good
+    _check(gi, oi, good, k=k, strategy=strat)
+    if bad:
+        with pytest.raises(gwa.GwaError, match="reference would abort"):
+            gwa.aligner(gi, gwa.AlignmentConfig(k=k, strategy=strat)).align_batch(good[:3] + bad[:1])
+    with pytest.raises(gwa.GwaError, match="512"):
+        gwa.aligner(gi, gwa.AlignmentConfig(k=k, strategy=strat)).align_batch([good[0], ("long", strs[0] * 2 + "A", None)])
+
+
+def test_reads_up_to_256_bp(random_pair):
+    """200 and 256 bp reads (QW = 8) align as the oracle does."""
+    codes, names, lengths, gi, oi = random_pair
+    for m in (200, 256):
+        seqs, rn = synth.reads(codes, lengths, 60, m, 2, config_id=7)
+        strs = synth.to_strings(seqs)
+        reads = []
+        for i, s_ in enumerate(strs):
+            try:
+                oi.align([(rn[i], s_, None)], O.OrcConfig.default(k=2.0))
+                reads.append((rn[i], s_, None))
+            except RuntimeError:
+                pass
+        _check(gi, oi, reads, k=2.0)
 
 
 def test_ecoli_c1_exact(gwa):

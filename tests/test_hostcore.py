@@ -250,3 +250,43 @@ def test_byte_parallel_to3bit_matches_acgt_table():
             got = L.hc_to3bit4(x)
             assert (got >> (8 * lane)) & 0xFF == table.get(b, 4), (b, lane)
             assert (got >> (8 * ((lane + 1) % 4))) & 0xFF == 2
+
+
+# ---- reads of 257..512 bp (QW = 16): read by read against the oracle, errors included ----
+
+def _long_cases():
+    codes, names, lengths = synth.genome([("chrA", 150000), ("chrB", 50000)], config_id=3)
+    return codes, names, lengths
+
+
+LONG_CASES = [(0, 257, 2.0), (0, 300, 5.0), (0, 333, 10.0), (0, 400, 2.0), (0, 480, 0.06), (0, 512, 31.0),
+              (1, 300, 31.0), (1, 333, 2.0), (1, 400, 5.0), (1, 400, 0.06), (1, 480, 5.0), (1, 512, 2.0)]
+
+
+@pytest.mark.parametrize("strategy,m,k", LONG_CASES)
+def test_long_reads_read_by_read(strategy, m, k):
+    """Above ~223 bp the reference's StaircaseFilter (byte) chunk starts wrap: some (m, minMismatches)
+    filters throw in their constructor (the run aborts where the reference builds that filter), others
+    give negative chunk starts and widths (-m sf seeds scanning nothing, staircase offsets outside
+    [-k, m]).  Each read alone: the host core reports the oracle's SAM, or fails where the oracle
+    throws."""
+    codes, names, lengths = _long_cases()
+    oi = O.Index.from_arrays(codes, names, lengths)
+    hc = hostcore.HostCore(codes, names, lengths)
+    seqs, rn = synth.reads(codes, lengths, 60, m, 3, config_id=4 + m)
+    strs = synth.to_strings(seqs)
+    errs = ok = 0
+    for i, s in enumerate(strs):
+        r = [("r%d" % i, s, "I" * m)]
+        try:
+            e = oi.align(r, O.OrcConfig.default(k=k, strategy=strategy))
+        except RuntimeError:
+            e = None
+        try:
+            g = hc.align(r, k=k, strategy=strategy)
+        except RuntimeError:
+            g = None
+        assert g == e, (m, k, strategy, i)
+        errs += e is None
+        ok += e is not None
+    assert ok > 0
