@@ -246,20 +246,87 @@ def host_ceiling_leg(args, gwa, synth, np, log, handles=4):
     pipe.close()
     for g in gis:
         g.close()
+    T, tdesc = host_cores()
+    procs = shard_processes_leg(np, synth, codes, names, lengths, d, fq, so, got, handles, log)
     for x in (fq, so):
         os.remove(x)
     os.rmdir(d)
-    T, tdesc = host_cores()
     out = {"reads_per_s": got / legs[1], "seconds": legs[1], "first_pass_seconds": legs[0], "reads": got,
            "handles": handles, "workers": 3 * handles, "host_cores": T, "sam_bytes": sam_bytes,
            "sam_GBps": sam_bytes / legs[1] / 1e9, "fastq_GBps": got * (2 * m + 15) / legs[1] / 1e9,
            "stages_s": {"read": pst.read_s, "frame": pst.frame_s, "setup": pst.setup_s,
                         "kernels": sum(pst.device_kernel_s[:handles]), "sam_format_d2h": pst.format_s,
                         "write": pst.write_s, "order_wait": pst.order_wait_s},
+           "two_processes": procs,
            "note": "FASTQ file -> SAM file through gwa_pipeline_align_file with %d index replicas (E. coli-size, "
                    "-k 0, exact reads) on one GPU: the host side's ceiling on %s; second pass" % (handles, tdesc)}
     log("host ceiling: %.1f M reads/s (%d handles, %.1f GB/s SAM out)" % (out["reads_per_s"] / 1e6, handles, out["sam_GBps"]))
     return out
+
+
+def shard_processes_leg(np, synth, codes, names, lengths, d, fq, one_sam, n, handles, log, nproc=2):
+    """detail.host_ceiling.two_processes: the same file through `nproc` processes at once, each running
+    `gwa align --shard r/nproc` (its contiguous shard of the file, its own SAM file: DESIGN.md §6's per-rank
+    sink) with handles / nproc index replicas; the rate is all reads over the slowest process's align
+    time (index load excluded, as above), and the shard files concatenated must equal the one-process SAM."""
+    import hashlib
+    import subprocess
+    ref = os.path.join(d, "ref.fa")
+    with open(ref, "w") as f:
+        f.write(synth.fasta_text(codes, names, lengths))
+    cli = os.path.join(REPO, "genome-weaver-align_amd", "gwa_cli.py")
+    per = max(1, handles // nproc)
+    outs, ps = [], []
+    t0 = time.perf_counter()
+    for r in range(nproc):
+        o = os.path.join(d, "shard%d.sam" % r)
+        outs.append(o)
+        with open(o, "wb") as fo:
+            ps.append(subprocess.Popen([sys.executable, cli, "align", "-r", ref, "-k", "0", "--devices", ",".join(["0"] * per),
+                                        "--workers", "3", "--timing", "--shard", "%d/%d" % (r, nproc), fq],
+                                       stdout=fo, stderr=subprocess.PIPE, text=True))
+    errs = [p.communicate()[1] for p in ps]
+    wall = time.perf_counter() - t0
+    align_s = []
+    for p, e in zip(ps, errs):
+        if p.returncode != 0:
+            return {"error": "shard process exited %d: %s" % (p.returncode, e[-400:])}
+        line = [x for x in e.splitlines() if "align (read file -> SAM" in x][-1]
+        align_s.append(float(line.split("index load excluded) ")[1].split("s")[0]))
+
+    def digest(paths):
+        h = hashlib.sha256()
+        for pth in paths:
+            with open(pth, "rb") as f:
+                for blk in iter(lambda: f.read(1 << 24), b""):
+                    h.update(blk)
+        return h.hexdigest()
+    # the one-process SAM has no header (pipeline output); shard 0 starts with the CLI's header
+    hdr = gwa_header_len(outs[0])
+    with open(outs[0], "rb") as f0, open(os.path.join(d, "shard0.body"), "wb") as fb:
+        f0.seek(hdr)
+        for blk in iter(lambda: f0.read(1 << 24), b""):
+            fb.write(blk)
+    same = digest([os.path.join(d, "shard0.body")] + outs[1:]) == digest([one_sam])
+    for x in outs + [os.path.join(d, "shard0.body"), ref]:
+        os.remove(x)
+    out = {"processes": nproc, "handles_per_process": per, "reads_per_s": n / max(align_s), "align_s": align_s,
+           "wall_s_incl_start_and_index": wall, "concatenation_identical_to_one_process": same,
+           "note": "gwa align --shard r/%d in %d processes on one GPU, each writing its own SAM shard" % (nproc, nproc)}
+    log("host ceiling, %d processes: %.1f M reads/s (align %s s), shards concatenated identical: %s"
+        % (nproc, out["reads_per_s"] / 1e6, ["%.2f" % x for x in align_s], same))
+    return out
+
+
+def gwa_header_len(path):
+    """bytes of the leading @SQ header lines of a SAM file"""
+    n = 0
+    with open(path, "rb") as f:
+        for line in f:
+            if not line.startswith(b"@"):
+                break
+            n += len(line)
+    return n
 
 
 def hg19r_leg(args, gen, gwa, synth, np, cfg, log):

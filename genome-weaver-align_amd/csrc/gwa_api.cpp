@@ -895,13 +895,13 @@ int gwa_batch_run(gwa_batch_t *b) {
     int t = 0, regrow = 0, launches = 0;
     // Reads that overflow the last tier rerun on it with the exceeded capacities doubled (OV_* bits
     // the kernel ORs into d_count[15]), as often as needed: no read the reference would finish is
-    // refused for capacity.  The hard limits are the state index of a queue entry (BsfLane KS: 2^16
-    // states on the BSF path, 2^24 on the SF path) and the scratch budget; past them the batch fails
-    // with the read count and the limit.  (BSF arenas are bounded by the search itself: <= 20m + 5
-    // FM steps each create <= 1 state and, with num_split = 1, <= 2 split states per state expanded,
-    // ~15.4k states for m = 255, well under 2^16.)
+    // refused for capacity.  The hard limits are the state index of a queue entry (2^24 states,
+    // BsfLane KS) and the scratch budget; past them the batch fails with the read count and the
+    // limit.  (BSF arenas are bounded by the search itself: <= 20m + 5 FM steps each create <= 1
+    // state and, with num_split = 1, <= 2 split states per state expanded: ~31k states for m = 512.
+    // The SF search has no such bound, S/SuffixFilter.java:257-290.)
     int gArena = 0, gHits = 0, gList = 0, gCigar = 0, gCand = 0;
-    const int arenaMaxLog = sf ? 24 : 16;
+    const int arenaMaxLog = 24;
     while (n > 0) {
       if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
       const int tb = std::min(t, kNumTiers - 1);  // t > kNumTiers - 1: the last tier, grown
@@ -912,7 +912,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       // GWA_TIER_ARENA="a0,a1,a2,a3": arena / heap states of tiers >= 1, and of tier 0 for the
       // hybrid-heap (k >= 4) kernels, whose heap is not bounded by the LDS array (tuning runs)
       if ((tb > 0 || b->R >= 8) && !sf) {
-        const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", tb, (uint32_t)T.arena), 65536u);
+        const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", tb, (uint32_t)T.arena), 1u << 24);
         caps.arena = caps.heap = a;
         caps.hits = caps.list = (int)tierValue("GWA_TIER_HITS", tb, (uint32_t)T.hits);  // hit list / report list
         caps.cigar = (int)tierValue("GWA_TIER_CIGAR", tb, (uint32_t)T.cigar);
@@ -935,34 +935,37 @@ int gwa_batch_run(gwa_batch_t *b) {
       caps.dpWords = 2 * bMax * (nref + 1);
       caps.path = m + nref + 8;
       caps.dpSlice = tb == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
-      const uint64_t stride = laneBytesFor(b->R, caps);
-      const uint64_t per = stride + ilvBytesFor(caps);
+      const uint64_t stride = laneBytesFor(b->R, caps), ilv = ilvBytesFor(caps);
       const uint64_t budget = scratchBudget(ix);
-      if (per * 256 > budget)
-        throw std::runtime_error(std::to_string(n) + " reads need more than " + std::to_string(budget >> 20) +
-                                 " MiB of search scratch per 256 lanes (" + std::to_string(caps.arena) +
-                                 " states per lane): the device memory budget is exhausted");
+      const uint64_t maxSparse = tierValue("GWA_SPARSE_LANES", 0, 262144u);
+      // scratch of `ln` lanes of which every sp-th takes reads: slices for the active ones, the
+      // interleaved DP block for all (bsf_search_kernel / sf_search_kernel addressing)
+      auto mem = [&](uint64_t st, uint64_t ln, uint64_t sp) { return st * (ln / sp) + ilv * ln; };
       uint32_t lanes = std::min<uint32_t>(n, tierValue("GWA_TIER_LANES", tb, T.maxLanes));
       lanes = (lanes + 255) / 256 * 256;
       // deep tiers: as many lanes as the scratch budget allows (at least one workgroup)
-      lanes = (uint32_t)std::min<uint64_t>(lanes, std::max<uint64_t>(256, budget / per / 256 * 256));
-      if (tb > 0) {
+      lanes = (uint32_t)std::min<uint64_t>(lanes, std::max<uint64_t>(256, budget / (stride + ilv) / 256 * 256));
+      if (tb > 0 && (!sf || tb == kNumTiers - 1)) {
         // a deep tier with few reads: 64 / s reads per wavefront (every s-th lane), the largest s
         // whose n x s lanes stay within GWA_SPARSE_LANES (default 262144) and the scratch budget
-        const uint64_t maxSparse = tierValue("GWA_SPARSE_LANES", 0, 262144u);
         for (uint32_t sp = 64; sp >= 2; sp /= 2) {
           const uint64_t sl = ((uint64_t)n * sp + 255) / 256 * 256;
-          if (sl <= maxSparse && sl * per <= budget && (!sf || tb == kNumTiers - 1)) {
+          if (sl <= maxSparse && mem(stride, sl, sp) <= budget) {
             lanes = (uint32_t)sl;
             caps.sparse = (int32_t)sp;
             break;
           }
         }
       }
+      const uint64_t spUsed = caps.sparse > 1 ? (uint64_t)caps.sparse : 1;
+      if (mem(stride, lanes, spUsed) > budget)
+        throw std::runtime_error(std::to_string(n) + " reads need more than the " + std::to_string(budget >> 20) +
+                                 " MiB search scratch budget (" + std::to_string(caps.arena) +
+                                 " states per lane): the device memory is exhausted");
       // a very sparse tier whose lanes fit one round of one workgroup per CU (256 CUs x 4 waves):
       // its queue tops go to LDS (bsf_search_kernel LH 2; the 64 KiB array leaves one workgroup per CU)
       const bool deepLds = !sf && tb > 0 && caps.sparse >= 8 && lanes <= 65536u;
-      const size_t need = (size_t)per * lanes;
+      const size_t need = (size_t)mem(stride, lanes, spUsed);
       if (need > ix->scratchBytes) {
         if (ix->scratch) HIPCHK(hipFree(ix->scratch));
         ix->scratch = nullptr;
@@ -1050,7 +1053,17 @@ int gwa_batch_run(gwa_batch_t *b) {
           if (lg >= arenaMaxLog)
             throw std::runtime_error(std::to_string(n) + " reads need more than 2^" + std::to_string(arenaMaxLog) +
                                      " search states (the queue-entry state index)");
+          // straight to the largest arena the scratch budget gives these reads (one read per
+          // wavefront when they are few), not one doubling per rerun: every rerun restarts the
+          // searches, and the -m sf searches on repeats queue up to millions of states
           ++gArena;
+          ++lg;
+          const uint64_t sp = n * 64 <= maxSparse ? 64 : 1, ln = ((uint64_t)n * sp + 255) / 256 * 256;
+          for (; lg < arenaMaxLog; ++lg, ++gArena) {
+            Caps c2 = caps;
+            c2.arena = c2.heap = 1 << (lg + 1);
+            if (mem(laneBytesFor(b->R, c2), ln, sp) > budget) break;
+          }
         }
         if (bits & OV_HITS) ++gHits;
         if (bits & OV_LIST) ++gList;

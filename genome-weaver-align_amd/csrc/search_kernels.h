@@ -65,9 +65,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
                                                          uint32_t *ovfBits, uint32_t *trace, int traceRead) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
-  // scratch = [lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]
-  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
-  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+  // scratch = [active lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]; a
+  // sparse tier (caps.sparse = s > 1: every s-th lane takes reads) has total / s active lanes
+  const uint32_t sp = caps.sparse > 1 ? (uint32_t)caps.sparse : 1u;
+  const uint32_t act = (gid >> 6) * (64u / sp) + (gid & 63) / sp;
+  uint8_t *chunk = scratch + (size_t)(total / sp) * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
+  LaneMem<R> L = laneMem<R>(scratch + (size_t)act * laneStride, chunk, (int)(gid & 63), 64, caps);
   // first tier: the priority queue lives in LDS, entry i of thread t at heapLds[i * 256 + t]
   // (heap high-water marks are ~5 entries for k <= 2, 100 bp; larger heaps overflow to tier 1)
   // LH 2: a sparse deep tier (caps.sparse >= 8, a few long searches, one workgroup per CU): each
@@ -217,8 +220,12 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
                  const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
-  uint8_t *chunk = scratch + (size_t)total * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
-  LaneMem<R> L = laneMem<R>(scratch + (size_t)gid * laneStride, chunk, (int)(gid & 63), 64, caps);
+  // scratch = [active lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]; a
+  // sparse tier (caps.sparse = s > 1: every s-th lane takes reads) has total / s active lanes
+  const uint32_t sp = caps.sparse > 1 ? (uint32_t)caps.sparse : 1u;
+  const uint32_t act = (gid >> 6) * (64u / sp) + (gid & 63) / sp;
+  uint8_t *chunk = scratch + (size_t)(total / sp) * laneStride + (size_t)(gid >> 6) * 64 * ilvBytes(caps);
+  LaneMem<R> L = laneMem<R>(scratch + (size_t)act * laneStride, chunk, (int)(gid & 63), 64, caps);
   __shared__ uint64_t stairLds[kStairLdsWords];
   if (st.ldsM >= 0) {
     for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
