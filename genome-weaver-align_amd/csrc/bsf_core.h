@@ -2077,16 +2077,18 @@ struct BsfLane {
       // children (:386-410): nextBase first -- a state from it ends the iteration -- then every
       // base still unchecked; one FM step per call
       GWA_PT(te);
-      int ch = -1, tt = xT;
+      int ch = -1, tt = xT, zero = 0;
       for (; tt < 4 && ch < 0; ++tt) {
-        // StaircaseFilter sf = getStairCaseFilter(m) before the loop over every base (:439)
-        if (tt == 0 && !stairOk()) return SS_DONE;
+        zero |= tt == 0 ? 1 : 0;  // (single-exit loop, integer state: see quickScan)
         const int cand = tt < 0 ? xNextBase : tt;
         if (xCS.state & (1 << cand)) continue;  // isChecked
         xCS.state |= 1 << cand;                 // updateFlag
         if (siIsEmpty(xCS, cand)) { storeStateWord(xC, xCS.state); continue; }
         ch = cand;
       }
+      // StaircaseFilter sf = getStairCaseFilter(m) where the loop over every base begins (:439); this
+      // micro-step entered it if it ran the loop at tt = 0
+      if (zero && !stairOk()) return SS_DONE;
       const int first = (xT < 0 && tt == 0) ? 1 : 0;  // the child taken is nextBase
       xT = tt;
       if (ch >= 0) {

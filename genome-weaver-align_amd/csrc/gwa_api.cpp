@@ -116,6 +116,11 @@ struct gwa_batch {
   uint32_t *d_row = nullptr, *d_seen = nullptr;
   void *d_encTmp = nullptr;
   size_t encTmpBytes = 0;
+  // the quick scan's read order (GWA_QS_SORT: reads sorted by their first k-mer), or none
+  uint32_t *d_qsKey = nullptr, *d_qsKey2 = nullptr, *d_qsIds = nullptr, *d_qsOrder = nullptr;
+  void *d_qsTmp = nullptr;
+  size_t qsTmpBytes = 0;
+  int qsBits = 0;
   // device
   uint8_t *d_codes = nullptr;
   uint32_t *d_off = nullptr, *d_len = nullptr;
@@ -494,7 +499,8 @@ static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
                 b->d_stair, b->d_stairBase, b->d_stairBad, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
-                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue, b->d_heavy};
+                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue, b->d_heavy,
+                b->d_qsKey, b->d_qsKey2, b->d_qsIds, b->d_qsOrder, b->d_qsTmp};
   for (void *p : ps)
     if (p) (void)hipFree(p);
   // the text blobs (one allocation may back several of them)
@@ -631,6 +637,18 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   b->d_list[0] = devAlloc<uint32_t>(n);
   b->d_list[1] = devAlloc<uint32_t>(n);
   b->d_count = devAlloc<uint32_t>(16);
+  if (cfg->strategy == 0 && b->ix->view.kmerK > 0) {
+    const char *e = getenv("GWA_QS_SORT");
+    b->qsBits = std::min(e ? atoi(e) : 0, 2 * b->ix->view.kmerK);
+    if (b->qsBits > 0) {
+      b->d_qsKey = devAlloc<uint32_t>(n);
+      b->d_qsKey2 = devAlloc<uint32_t>(n);
+      b->d_qsIds = devAlloc<uint32_t>(n);
+      b->d_qsOrder = devAlloc<uint32_t>(n);
+      b->qsTmpBytes = qsOrderTempBytes(n);
+      b->d_qsTmp = devAlloc<uint8_t>(b->qsTmpBytes);
+    }
+  }
   if (cfg->strategy == 1) {
     std::vector<uint32_t> all(n);
     for (uint32_t i = 0; i < n; ++i) all[i] = i;
@@ -875,9 +893,12 @@ int gwa_batch_run(gwa_batch_t *b) {
     HIPCHK(hipMemsetAsync(b->d_count, 0, 16 * sizeof(uint32_t), s));
     HIPCHK(hipEventRecord(e0, s));
     const bool sf = b->cfg.strategy == 1;
+    if (!sf && b->qsBits > 0)
+      launchQsOrder(rv, ix->view.kmerK, b->qsBits, b->d_qsKey, b->d_qsKey2, b->d_qsIds, b->d_qsOrder, b->d_qsTmp,
+                    b->qsTmpBytes, s);
     if (!sf)
       launchQuickscan(qwFor(b->maxM), ix->view, b->scfg, rv, b->d_sres, b->d_oh, outSlots(b), b->d_list[0],
-                      b->d_count, s);
+                      b->d_count, b->qsBits > 0 ? b->d_qsOrder : nullptr, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
     uint32_t nSearch = b->n;
@@ -1062,7 +1083,7 @@ int gwa_batch_run(gwa_batch_t *b) {
           for (; lg < arenaMaxLog; ++lg, ++gArena) {
             Caps c2 = caps;
             c2.arena = c2.heap = 1 << (lg + 1);
-            if (mem(laneBytesFor(b->R, c2), ln, sp) > budget) break;
+            if (mem(laneBytesFor(b->R, c2), ln, sp) > budget / 2) break;
           }
         }
         if (bits & OV_HITS) ++gHits;
@@ -1096,13 +1117,15 @@ int gwa_batch_run(gwa_batch_t *b) {
       }
       uint32_t *heavyCount = b->d_heavy + b->pairs;
       HIPCHK(hipEventRecord(e1, s));
-      HIPCHK(hipMemsetAsync(heavyCount, 0, 4, s));
+      HIPCHK(hipMemsetAsync(heavyCount, 0, 8, s));
       launchPairRescue(lanes, ix->view, b->scfg, b->st, rv, samText(b), b->d_oh, b->d_hits, b->d_cig, b->pairs, b->minIns,
                        b->maxIns, ix->scratch, stride, rc, b->d_rescue,
                        getenv("GWA_PAIR_QUAD") ? atol(getenv("GWA_PAIR_QUAD")) : kPairQuad, b->d_heavy, heavyCount, s);
       HIPCHK(hipGetLastError());
-      uint32_t nHeavy = 0;
-      HIPCHK(hipMemcpyAsync(&nHeavy, heavyCount, 4, hipMemcpyDeviceToHost, s));
+      uint32_t hc[2] = {0, 0};
+      HIPCHK(hipMemcpyAsync(hc, heavyCount, 8, hipMemcpyDeviceToHost, s));
+      const uint32_t nHeavy = hc[0];
+      b->stats.rescue_window_skipped = hc[1];
       HIPCHK(hipStreamSynchronize(s));
       if (nHeavy > b->pairs) throw std::runtime_error("pair choice: heavy-pair count out of range");
       launchPairChoose(nHeavy, samText(b), b->d_oh, b->d_hits, b->d_cig, b->pairs, b->minIns, b->maxIns, b->d_heavy,
@@ -1117,6 +1140,14 @@ int gwa_batch_run(gwa_batch_t *b) {
     }
     b->stats.rescue_ms = rescueMs;
     b->stats.kernel_ms = ems + qms + searchMs + rescueMs;
+    // a grown last tier may have taken tens of GiB of scratch for a few reads: give it back rather
+    // than hold it for the index's life (the next batch allocates what its tiers need)
+    if (t > kNumTiers) {
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipFree(ix->scratch));
+      ix->scratch = nullptr;
+      ix->scratchBytes = 0;
+    }
     b->ran = true;
     return 0;
   } catch (std::exception &e) {
@@ -1411,7 +1442,7 @@ int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_r
     (*out)->minIns = min_insert;
     (*out)->maxIns = max_insert;
     (*out)->d_rescue = devAlloc<RescueOut>(n);
-    (*out)->d_heavy = devAlloc<uint32_t>((size_t)n + 1);
+    (*out)->d_heavy = devAlloc<uint32_t>((size_t)n + 2);  // list, its count, rescues skipped (window)
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());

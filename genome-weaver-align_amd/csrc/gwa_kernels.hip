@@ -83,6 +83,7 @@ __global__ void __launch_bounds__(64) pair_rescue_kernel(IndexView ix, SearchCon
             }
             ws = ws > off ? ws : off;
             we = we < off + clen ? we : off + clen;
+            if (we - ws > kRescueWindow) atomicAdd(heavyCount + 1, 1u);  // rule 3 not applied (gwa.h)
             if (we - ws >= m && we - ws <= kRescueWindow) {
               int pos = 0, diff = 0, co = 0, cl = 0;
               const int res = lane.alignBlockDetailed(strand, 0, m, ws, we, &pos, &diff, &co, &cl);
@@ -290,12 +291,12 @@ void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream
 }
 
 void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount,
+                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order,
                      hipStream_t s, uint32_t *trace, int traceRead) {
   if (reads.n == 0) return;
-  if (QW == 4) launchQuickscanT<4>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
-  else if (QW == 8) launchQuickscanT<8>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
-  else launchQuickscan16(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
+  if (QW == 4) launchQuickscanT<4>(ix, cfg, reads, sres, oh, os, searchList, searchCount, order, s, trace, traceRead);
+  else if (QW == 8) launchQuickscanT<8>(ix, cfg, reads, sres, oh, os, searchList, searchCount, order, s, trace, traceRead);
+  else launchQuickscan16(ix, cfg, reads, sres, oh, os, searchList, searchCount, order, s, trace, traceRead);
 }
 
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,

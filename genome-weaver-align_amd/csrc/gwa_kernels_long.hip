@@ -6,9 +6,9 @@
 namespace gwa {
 
 void launchQuickscan16(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
-                       int traceRead) {
-  launchQuickscanT<16>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
+                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order,
+                       hipStream_t s, uint32_t *trace, int traceRead) {
+  launchQuickscanT<16>(ix, cfg, reads, sres, oh, os, searchList, searchCount, order, s, trace, traceRead);
 }
 
 void launchSearch16(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,

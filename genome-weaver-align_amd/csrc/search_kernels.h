@@ -28,11 +28,14 @@ __device__ __forceinline__ void waveAppend(bool need, uint32_t value, uint32_t *
 template <int QW>
 __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
                                                            OutHeader *oh, OutSlots os,
-                                                           uint32_t *searchList, uint32_t *searchCount, uint32_t *trace,
-                                                           int traceRead) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+                                                           uint32_t *searchList, uint32_t *searchCount,
+                                                           const uint32_t *order, uint32_t *trace, int traceRead) {
+  // lane i scans read order[i] (reads sorted by their first k-mer: neighbouring lanes start on
+  // neighbouring suffix-array rows, gwa_batch_run) or read i
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t r = (order && i < reads.n) ? order[i] : i;
   bool need = false;
-  if (r < reads.n) {
+  if (i < reads.n) {
     const uint32_t o = reads.off[r];
     const int m = (int)reads.len[r];
     OutHeader *h = oh + r;
@@ -283,10 +286,10 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
 
 template <int QW>
 void launchQuickscanT(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
-                      int traceRead) {
+                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order, hipStream_t s,
+                      uint32_t *trace, int traceRead) {
   hipLaunchKernelGGL(fm_quickscan_kernel<QW>, dim3((reads.n + 255) / 256), dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
-                     searchList, searchCount, trace, traceRead);
+                     searchList, searchCount, order, trace, traceRead);
 }
 
 template <int QW>
@@ -337,8 +340,8 @@ void launchSfSearchT(int R, uint32_t lanes, const IndexView &ix, const SearchCon
 
 // the QW = 16 instances (gwa_kernels_long.hip)
 void launchQuickscan16(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
-                       int traceRead);
+                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order,
+                       hipStream_t s, uint32_t *trace, int traceRead);
 void launchSearch16(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                     const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                     uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank,

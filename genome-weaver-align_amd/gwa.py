@@ -59,7 +59,8 @@ class BatchStats(ctypes.Structure):
                 ("search_short_steps", ctypes.c_uint64), ("tier_ms", ctypes.c_float * 4),
                 ("num_sw", ctypes.c_uint64), ("verify_bytes", ctypes.c_uint64),
                 ("quick_text_runs", ctypes.c_uint64), ("encode_ms", ctypes.c_double), ("format_ms", ctypes.c_double),
-                ("rescue_ms", ctypes.c_double), ("heavy_pairs", ctypes.c_uint64)]
+                ("rescue_ms", ctypes.c_double), ("heavy_pairs", ctypes.c_uint64),
+                ("rescue_window_skipped", ctypes.c_uint64)]
 
 
 def shard_range(path, shard, nshards):

@@ -123,7 +123,9 @@ def build_parser():
     a.add_argument("--batch", type=int, default=1 << 20, help="reads per device batch")
     a.add_argument("--timing", action="store_true", help="index / align wall times and reads/s on stderr")
     a.add_argument("--insert-min", type=int, default=210, help="paired-end: smallest template length of a proper pair")
-    a.add_argument("--insert-max", type=int, default=390, help="paired-end: largest template length of a proper pair")
+    a.add_argument("--insert-max", type=int, default=390,
+                   help="paired-end: largest template length of a proper pair (mate rescue needs max - min + read "
+                        "length + 2k <= 320 bases; wider ranges pair without rescue)")
     a.add_argument("--shard", default=None, metavar="R/N",
                    help="one process per GPU: align contiguous shard R of N of the (plain) read file; the SAM "
                         "header is written by shard 0 only, so the shards' outputs concatenated in order are "

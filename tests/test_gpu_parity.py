@@ -308,6 +308,22 @@ def test_many_equal_hits_on_gpu(many_hits_pair, strategy, rt):
     assert genomes.max_lines_per_read(sam) >= 5
 
 
+@pytest.mark.parametrize("stage", ["1024", "4096"])
+def test_sam_writer_direct_write_fallback(many_hits_pair, random_pair, monkeypatch, stage):
+    # samWriteKernel stages a workgroup's 64 records in LDS and writes them out in 16-B chunks; a
+    # workgroup whose records do not fit writes them directly, next to staged neighbours that write
+    # the shared edge chunks bytewise.  A small staging buffer (GWA_SAM_STAGE) sends the many-hit reads'
+    # workgroups (hundreds of lines) and, at 1024 B, every workgroup down the direct path: same bytes
+    gi, oi, reads = many_hits_pair
+    monkeypatch.setenv("GWA_SAM_STAGE", stage)
+    _check(gi, oi, reads, k=5.0, reportType="allhits")
+    codes, names, lengths, gi2, oi2 = random_pair
+    seqs, rn = synth.reads(codes, lengths, 700, 100, 2, config_id=31)
+    strs = synth.to_strings(seqs)
+    mix = [(rn[i], strs[i][: 10 + (i * 37) % 91], None if i % 3 else "I" * (10 + (i * 37) % 91)) for i in range(700)]
+    _check(gi2, oi2, mix, k=2.0)
+
+
 def test_output_pool_growth(many_hits_pair, monkeypatch):
     # a 4-hit initial pool: the reads that overflow it are rerun after the pool grows
     gi, oi, reads = many_hits_pair
