@@ -37,7 +37,7 @@ def log(*a):
 
 
 def _pmc_traffic(kernel, workload):
-    """Per-launch HBM read bytes of `kernel` from the newest committed rocprofv3 PMC summary of the
+    """Per-launch HBM read (+ write, when measured) bytes of `kernel` from the newest committed rocprofv3 PMC summary of the
     same workload (profiles/*_profile.json, written by tools/prof_summary.py from FETCH_SIZE, see
     profiles/README.md for the correction); (None, None) when no profile of this workload exists.
     "Newest" is by round tag in the file name (r01 < r01c < r01d ...): file mtimes do not survive a
@@ -52,7 +52,8 @@ def _pmc_traffic(kernel, workload):
         except (OSError, ValueError, KeyError):
             continue
         if line.get("config", {}).get("workload") == workload and "hbm_read_bytes_corrected" in k:
-            best = (k["hbm_read_bytes_corrected"], os.path.relpath(f, REPO))
+            # read + write fabric request bytes when the profile has a WRITE_SIZE pass (round 4 on)
+            best = (k["hbm_read_bytes_corrected"] + k.get("hbm_write_bytes", 0.0), os.path.relpath(f, REPO))
     return best if best else (None, None)
 
 

@@ -17,7 +17,6 @@
 // Also here: the batch statistics as a device reduction over the per-read output headers.
 #include <hip/hip_runtime.h>
 
-#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include <cstdlib>
@@ -164,40 +163,6 @@ size_t encodeScanTempBytes(uint32_t n) {
   FCHK(rocprim::exclusive_scan(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t)0, (size_t)n + 1,
                                rocprim::plus<uint32_t>(), (hipStream_t)0));
   return b;
-}
-
-// ---- the quick scan's read order ----
-// Key of read r: its first K codes (N as A, replaceN_withA), first base in the low bits -- the k-mer
-// table's key (IndexView::kmer), whose numeric order is the suffix-array order of the interval the
-// quick scan's first lookup reaches on strand 0 (the first base is the last one prepended by the
-// backward steps, i.e. the most significant character of the suffix).
-__global__ void __launch_bounds__(256) qsKeyKernel(ReadsView reads, int K, uint32_t *keys, uint32_t *ids) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= reads.n) return;
-  const uint8_t *c = reads.codes + reads.off[r];
-  const int m = (int)reads.len[r];
-  uint32_t key = 0;
-  for (int j = 0; j < K && j < m; ++j) {
-    const uint32_t x = c[j];
-    key |= (x > 3 ? 0u : x) << (2 * j);
-  }
-  keys[r] = key;
-  ids[r] = r;
-}
-
-size_t qsOrderTempBytes(uint32_t n) {
-  size_t b = 0;
-  FCHK(rocprim::radix_sort_pairs(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                 (uint32_t *)nullptr, (size_t)n, 0, 32, (hipStream_t)0));
-  return b;
-}
-
-void launchQsOrder(const ReadsView &reads, int K, int bits, uint32_t *keys, uint32_t *keys2, uint32_t *ids, uint32_t *order,
-                   void *tmp, size_t tmpBytes, hipStream_t s) {
-  if (reads.n == 0) return;
-  hipLaunchKernelGGL(qsKeyKernel, dim3((reads.n + 255) / 256), dim3(256), 0, s, reads, K, keys, ids);
-  const int hi = 2 * K, lo = hi - bits > 0 ? hi - bits : 0;
-  FCHK(rocprim::radix_sort_pairs(tmp, tmpBytes, keys, keys2, ids, order, (size_t)reads.n, (unsigned)lo, (unsigned)hi, s));
 }
 
 // FASTQ records straight from the file text (the pipeline's zero-copy path): record r starts at

@@ -116,11 +116,6 @@ struct gwa_batch {
   uint32_t *d_row = nullptr, *d_seen = nullptr;
   void *d_encTmp = nullptr;
   size_t encTmpBytes = 0;
-  // the quick scan's read order (GWA_QS_SORT: reads sorted by their first k-mer), or none
-  uint32_t *d_qsKey = nullptr, *d_qsKey2 = nullptr, *d_qsIds = nullptr, *d_qsOrder = nullptr;
-  void *d_qsTmp = nullptr;
-  size_t qsTmpBytes = 0;
-  int qsBits = 0;
   // device
   uint8_t *d_codes = nullptr;
   uint32_t *d_off = nullptr, *d_len = nullptr;
@@ -499,8 +494,7 @@ static void freeBatchDev(gwa_batch *b) {
   void *ps[] = {b->d_codes, b->d_off, b->d_len, b->d_sres, b->d_oh, b->d_hits, b->d_cig, b->d_list[0], b->d_list[1], b->d_all, b->d_count,
                 b->d_stair, b->d_stairBase, b->d_stairBad, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
-                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue, b->d_heavy,
-                b->d_qsKey, b->d_qsKey2, b->d_qsIds, b->d_qsOrder, b->d_qsTmp};
+                b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue, b->d_heavy};
   for (void *p : ps)
     if (p) (void)hipFree(p);
   // the text blobs (one allocation may back several of them)
@@ -637,18 +631,6 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   b->d_list[0] = devAlloc<uint32_t>(n);
   b->d_list[1] = devAlloc<uint32_t>(n);
   b->d_count = devAlloc<uint32_t>(16);
-  if (cfg->strategy == 0 && b->ix->view.kmerK > 0) {
-    const char *e = getenv("GWA_QS_SORT");
-    b->qsBits = std::min(e ? atoi(e) : 0, 2 * b->ix->view.kmerK);
-    if (b->qsBits > 0) {
-      b->d_qsKey = devAlloc<uint32_t>(n);
-      b->d_qsKey2 = devAlloc<uint32_t>(n);
-      b->d_qsIds = devAlloc<uint32_t>(n);
-      b->d_qsOrder = devAlloc<uint32_t>(n);
-      b->qsTmpBytes = qsOrderTempBytes(n);
-      b->d_qsTmp = devAlloc<uint8_t>(b->qsTmpBytes);
-    }
-  }
   if (cfg->strategy == 1) {
     std::vector<uint32_t> all(n);
     for (uint32_t i = 0; i < n; ++i) all[i] = i;
@@ -893,12 +875,9 @@ int gwa_batch_run(gwa_batch_t *b) {
     HIPCHK(hipMemsetAsync(b->d_count, 0, 16 * sizeof(uint32_t), s));
     HIPCHK(hipEventRecord(e0, s));
     const bool sf = b->cfg.strategy == 1;
-    if (!sf && b->qsBits > 0)
-      launchQsOrder(rv, ix->view.kmerK, b->qsBits, b->d_qsKey, b->d_qsKey2, b->d_qsIds, b->d_qsOrder, b->d_qsTmp,
-                    b->qsTmpBytes, s);
     if (!sf)
       launchQuickscan(qwFor(b->maxM), ix->view, b->scfg, rv, b->d_sres, b->d_oh, outSlots(b), b->d_list[0],
-                      b->d_count, b->qsBits > 0 ? b->d_qsOrder : nullptr, s);
+                      b->d_count, nullptr, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
     uint32_t nSearch = b->n;

@@ -13,12 +13,6 @@ struct Caps;
 void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order,
                      hipStream_t s, uint32_t *trace = nullptr, int traceRead = -1);
-// the quick scan's read order: reads sorted by the top `bits` bits of their first K-mer key (strand
-// 0, N as A; K = the index's k-mer table k), the order of the suffix intervals the scan's first lookup
-// reaches.  keys / ids / order: n entries each; tmp: qsOrderTempBytes(n) bytes
-size_t qsOrderTempBytes(uint32_t n);
-void launchQsOrder(const ReadsView &reads, int K, int bits, uint32_t *keys, uint32_t *keys2, uint32_t *ids, uint32_t *order,
-                   void *tmp, size_t tmpBytes, hipStream_t s);
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                   uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,

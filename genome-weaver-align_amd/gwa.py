@@ -13,6 +13,9 @@ import os
 from dataclasses import dataclass, fields
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# A process that also uses torch on the GPU must import torch before this library loads: torch's bundled
+# HIP runtime and the system ROCm one libgwa.so links have the same SONAME (libamdhip64.so.7), so the
+# first one loaded serves both, and torch initialises its device only on its own.
 LIBPATH = os.path.join(_HERE, os.environ.get("GWA_LIB", "libgwa.so"))  # GWA_LIB=libgwa_prof.so: profiling build
 
 

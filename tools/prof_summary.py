@@ -92,7 +92,8 @@ def summarise(d):
     # PMC passes: average per dispatch of each counter
     # (the PMC passes run bench.py --check 0 --no-pipeline: only the timed region's dispatches are
     # kept when its window is known)
-    for sub, bl in [("pmc_fetch", "bench_pmc1.json"), ("pmc_sq", "bench_pmc2.json"), ("pmc_tcc", "bench_pmc3.json")]:
+    for sub, bl in [("pmc_fetch", "bench_pmc1.json"), ("pmc_sq", "bench_pmc2.json"), ("pmc_tcc", "bench_pmc3.json"),
+                    ("pmc_write", "bench_pmc4.json")]:
         acc = {}
         keep = _timed_ids(d, sub, _window(d, bl))
         for r in _rows(os.path.join(d, sub, "**", "*_counter_collection.csv")):
@@ -112,6 +113,8 @@ def summarise(d):
         if "FETCH_SIZE" in p:
             e["hbm_read_bytes_corrected"] = 1024.0 * p["FETCH_SIZE"]
             e["hbm_read_bytes_stream_x2"] = 2.0 * 1024.0 * p["FETCH_SIZE"]
+        if "WRITE_SIZE" in p:  # KiB of fabric write requests (uncalibrated for scattered 8/16-B stores)
+            e["hbm_write_bytes"] = 1024.0 * p["WRITE_SIZE"]
         if "TCC_HIT_sum" in p and "TCC_MISS_sum" in p and p["TCC_HIT_sum"] + p["TCC_MISS_sum"] > 0:
             e["l2_hit_rate"] = p["TCC_HIT_sum"] / (p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
         if "SQ_WAIT_ANY" in p and p.get("SQ_WAVE_CYCLES"):
