@@ -203,7 +203,11 @@ struct Caps {
   int32_t dpSlice;  // 1: the DP history keeps a 32-row slice around the read's diagonal (first tier)
   int32_t cand;  // SuffixFilter candidate set (sf_core.h); 0 on the BSF path
   int32_t sparse;  // > 1: only every sparse-th lane of a wavefront takes reads (deep tiers, bsf_search_kernel)
+  int32_t sf;      // 1: the arena holds SfState<R> (sf_core.h), else DState<R>
 };
+// bytes of one arena slot: SfState<R> is 24 + 8 R bytes (static_assert in sf_core.h)
+template <int R>
+GWA_HD size_t stateBytes(const Caps &c) { return c.sf ? (size_t)(24 + 8 * R) : sizeof(DState<R>); }
 
 // Per-lane scratch.  The search structures (arena/heap/hits/list/cigar) sit in a per-lane slice;
 // the DP history, the per-column DP flags and the traceback path are "interleaved": element e of
@@ -238,7 +242,7 @@ struct LaneMem {
 template <int R>
 GWA_HD size_t laneBytes(const Caps &c) {  // per-lane slice
   size_t b = 0;
-  b += sizeof(DState<R>) * (size_t)c.arena;
+  b += stateBytes<R>(c) * (size_t)c.arena;
   b += 8 * (size_t)c.heap;
   b += 8 * (size_t)c.cand;
   b += sizeof(DHit) * (size_t)c.hits;
@@ -255,7 +259,7 @@ GWA_HD size_t ilvBytes(const Caps &c) {  // interleaved bytes per lane
 template <int R>
 GWA_HD LaneMem<R> laneMem(uint8_t *slice, uint8_t *chunk, int laneInWave, int is, const Caps &c) {
   LaneMem<R> L;
-  size_t b = sizeof(DState<R>) * (size_t)c.arena;
+  size_t b = stateBytes<R>(c) * (size_t)c.arena;
   L.slice = slice;
   L.oHeap = (uint32_t)b; b += 8 * (size_t)c.heap;
   L.oCand = (uint32_t)b; b += 8 * (size_t)c.cand;

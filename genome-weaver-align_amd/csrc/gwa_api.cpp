@@ -901,7 +901,9 @@ int gwa_batch_run(gwa_batch_t *b) {
     // state and, with num_split = 1, <= 2 split states per state expanded: ~31k states for m = 512.
     // The SF search has no such bound, S/SuffixFilter.java:257-290.)
     int gArena = 0, gHits = 0, gList = 0, gCigar = 0, gCand = 0;
-    const int arenaMaxLog = 24;
+    int arenaMaxLog = 24;
+    if (const char *e = getenv("GWA_MAX_STATES_LOG2"))  // diagnostics (tools/diag_sf.py): a lower state limit
+      arenaMaxLog = std::max(16, std::min(24, atoi(e)));
     while (n > 0) {
       if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
       const int tb = std::min(t, kNumTiers - 1);  // t > kNumTiers - 1: the last tier, grown
@@ -918,6 +920,7 @@ int gwa_batch_run(gwa_batch_t *b) {
         caps.cigar = (int)tierValue("GWA_TIER_CIGAR", tb, (uint32_t)T.cigar);
       }
       caps.cand = T.cand;
+      caps.sf = sf ? 1 : 0;
       if (tb == kNumTiers - 1) {  // the grown last tier
         caps.arena <<= gArena;
         caps.heap <<= gArena;
@@ -957,11 +960,20 @@ int gwa_batch_run(gwa_batch_t *b) {
           }
         }
       }
-      const uint64_t spUsed = caps.sparse > 1 ? (uint64_t)caps.sparse : 1;
-      if (mem(stride, lanes, spUsed) > budget)
-        throw std::runtime_error(std::to_string(n) + " reads need more than the " + std::to_string(budget >> 20) +
-                                 " MiB search scratch budget (" + std::to_string(caps.arena) +
-                                 " states per lane): the device memory is exhausted");
+      uint64_t spUsed = caps.sparse > 1 ? (uint64_t)caps.sparse : 1;
+      if (mem(stride, lanes, spUsed) > budget) {
+        // fewer active lanes than reads: the persistent lanes take the reads from the shared counter,
+        // as many at once as the budget holds (deep tiers: one read per wavefront)
+        if (tb > 0 && spUsed == 1) {
+          caps.sparse = 64;
+          spUsed = 64;
+        }
+        lanes = (uint32_t)std::min<uint64_t>(lanes, budget / (stride + ilv * spUsed) * spUsed / 256 * 256);
+        if (lanes < 256)
+          throw std::runtime_error(std::to_string(n) + " reads need more than the " + std::to_string(budget >> 20) +
+                                   " MiB search scratch budget (" + std::to_string(caps.arena) +
+                                   " states per lane): the device memory is exhausted");
+      }
       // a very sparse tier whose lanes fit one round of one workgroup per CU (256 CUs x 4 waves):
       // its queue tops go to LDS (bsf_search_kernel LH 2; the 64 KiB array leaves one workgroup per CU)
       const bool deepLds = !sf && tb > 0 && caps.sparse >= 8 && lanes <= 65536u;
@@ -1058,11 +1070,12 @@ int gwa_batch_run(gwa_batch_t *b) {
           // searches, and the -m sf searches on repeats queue up to millions of states
           ++gArena;
           ++lg;
-          const uint64_t sp = n * 64 <= maxSparse ? 64 : 1, ln = ((uint64_t)n * sp + 255) / 256 * 256;
+          const uint64_t conc = std::min<uint64_t>(n, 256);  // reads searching at once, at least
+          const uint64_t ln = (conc * 64 + 255) / 256 * 256;
           for (; lg < arenaMaxLog; ++lg, ++gArena) {
             Caps c2 = caps;
             c2.arena = c2.heap = 1 << (lg + 1);
-            if (mem(laneBytesFor(b->R, c2), ln, sp) > budget / 2) break;
+            if (mem(laneBytesFor(b->R, c2), ln, 64) > budget / 2) break;
           }
         }
         if (bits & OV_HITS) ++gHits;

@@ -25,7 +25,8 @@ struct SfState {
   uint8_t meta, pad[3];
   uint64_t nfa[R];
 };
-static_assert(sizeof(SfState<4>) <= sizeof(DState<4>), "SfState must fit the DState arena slots");
+static_assert(sizeof(SfState<4>) == 24 + 8 * 4 && sizeof(SfState<8>) == 24 + 8 * 8 && sizeof(SfState<32>) == 24 + 8 * 32,
+              "SfState size must match stateBytes (bsf_core.h)");
 
 template <int R, int QW>
 struct SfLane : BsfLane<R, QW, false, 24> {

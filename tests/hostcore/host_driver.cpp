@@ -37,9 +37,9 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
   const Caps tiers[4] = {{256, R >= 8 ? 256 : kLdsHeap, 32, 32, 512, dpw, path, sl, 0}, {1024, 1024, 64, 64, 1024, dpw, path, 0, 0},
                          {4096, 4096, 256, 256, 4096, dpw, path, 0, 0}, {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 0}};
   // -m sf tiers (gwa_api.cpp kSfTiers)
-  const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, sl, 32}, {2048, 2048, 64, 64, 2048, dpw, path, 0, 256},
-                           {8192, 8192, 256, 256, 4096, dpw, path, 0, 1024},
-                           {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 16384}};
+  const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, sl, 32, 0, 1}, {2048, 2048, 64, 64, 2048, dpw, path, 0, 256, 0, 1},
+                           {8192, 8192, 256, 256, 4096, dpw, path, 0, 1024, 0, 1},
+                           {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 16384, 0, 1}};
   std::vector<uint8_t> scratch(std::max(laneBytes<R>(tiers[3]), laneBytes<R>(sfTiers[3])) + ilvBytes(tiers[3]) + 4096);
   // one read at a time: a one-slot OutSlots whose pool is large enough for any report
   const int chains = cfg.reportType == 0 ? 1 : 2;

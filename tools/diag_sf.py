@@ -1,9 +1,12 @@
-"""Diagnostic (GPU box): -m sf (or bsf) at k = 5 on the full-size hg19-like genome -- per-tier reads
-and times, the heaviest reads (states created, FM searches, tier), then the oracle on every read that
-needed a tier >= 1, one at a time, with its state count and time, SAM compared.
+"""Diagnostic (GPU box): -m sf (or bsf) at k = 5 on the full-size hg19-like genome.  Runs a batch of C4
+reads (per-tier reads and times with GWA_VERBOSE=1), then -- whether or not the batch finished --
+the oracle on the heaviest reads, each in a child process with a state cap (ORC_MAX_STATES) and a
+time limit, to show how far the reference algorithm gets on them; then the oracle on every read
+that needed a tier >= 1 when the batch finished, SAM compared.
 
-  python tools/diag_sf.py [reads] [strategy] [oracle: 0/1]
+  python tools/diag_sf.py [reads] [strategy] [oracle reads] [state cap]
 """
+import multiprocessing as mp
 import os
 import sys
 import time
@@ -30,11 +33,28 @@ def heartbeat():
     threading.Thread(target=beat, daemon=True).start()
 
 
+_ORC = {}
+
+
+def _orc_one(args):
+    """child process: one read through the oracle with the state cap; (seconds, error or None, stats)"""
+    read, strat, cap = args
+    import oracle as O
+    os.environ["ORC_MAX_STATES"] = str(cap)
+    t0 = time.time()
+    try:
+        _, st = _ORC["oi"].align([read], O.OrcConfig.default(k=5.0, strategy=strat), with_stats=True)
+        return time.time() - t0, None, (st[0].states, st[0].fm_searches, st[0].sw, st[0].max_heap)
+    except RuntimeError as e:
+        return time.time() - t0, str(e), None
+
+
 def main():
     heartbeat()
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
     strat = sys.argv[2] if len(sys.argv) > 2 else "sf"
-    run_oracle = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    n_orc = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+    cap = int(sys.argv[4]) if len(sys.argv) > 4 else 20_000_000
     t0 = time.time()
     codes, names, lengths = synth.genome_repeats(synth.HG19_CONTIGS, config_id=1)
     say("genome %.0fs" % (time.time() - t0))
@@ -44,44 +64,50 @@ def main():
     reads = [("r%09d" % i, strs[i], "I" * 150) for i in range(n)]
     b = gwa.Batch(gi, gwa.AlignmentConfig(k=5.0, strategy=strat), reads)
     t1 = time.time()
-    b.run()
+    ok = True
+    try:
+        b.run()
+    except gwa.GwaError as e:
+        ok = False
+        say("batch failed after %.1fs: %s" % (time.time() - t1, e))
     st = b.stats()
     c = b.read_counters()
-    say("%s %d reads: %.2fs tiers %s tier_ms %s search %.1f ms fm/read %.0f states max %d fm max %d" % (
-        strat, n, time.time() - t1, list(st.tier_reads), [round(x) for x in st.tier_ms], st.search_ms,
-        st.fm_searches / n, c[:, 5].max(), c[:, 1].max()))
+    say("%s %d reads: %.2fs tiers %s tier_ms %s" % (strat, n, time.time() - t1, list(st.tier_reads),
+                                                   [round(x) for x in st.tier_ms]))
+    say("deepest tier per read:", {int(t): int((c[:, 12] == t).sum()) for t in np.unique(c[:, 12])})
     deep = np.nonzero(c[:, 12] >= 1)[0]
-    say("tier histogram:", {int(t): int((c[:, 12] == t).sum()) for t in np.unique(c[:, 12])})
-    top = np.argsort(-c[:, 5])[:12]
-    say("heaviest reads (read, fm searches, states, tier):", [(int(i), int(c[i, 1]), int(c[i, 5]), int(c[i, 12])) for i in top])
-    got, _ = b.results_select(deep.astype(np.uint32))
+    if ok:
+        top = np.argsort(-c[:, 5])[:12]
+        say("heaviest reads (read, fm searches, states, tier):", [(int(i), int(c[i, 1]), int(c[i, 5]), int(c[i, 12])) for i in top])
+        got, _ = b.results_select(deep.astype(np.uint32))
+    heavy = [int(i) for i in np.argsort(-c[:, 12], kind="stable")[:n_orc]]
     b.close()
-    if not run_oracle or len(deep) == 0:
-        return
     import oracle as O
     t0 = time.time()
     sa_f = gi.suffixArray(0)
     O.check_cyclic_sa_full(codes, sa_f, threads=16)
     sa_r = gi.suffixArray(1)
     O.check_cyclic_sa_full(np.ascontiguousarray(codes[::-1]), sa_r, threads=16)
-    oi = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
+    _ORC["oi"] = O.Index.from_arrays(codes, names, lengths, sa_f=sa_f, sa_r=sa_r)
     del sa_f, sa_r
+    gi.close()
     say("SA check + oracle index %.0fs" % (time.time() - t0))
-    cfg = O.OrcConfig.default(k=5.0, strategy=gwa.STRATEGIES[strat])
-    lines = got.splitlines(True)
-    order = np.argsort(-c[deep, 5])
-    heavy = [int(deep[j]) for j in order[:16]]
-    for r in heavy:
+    strat_i = gwa.STRATEGIES[strat]
+    ctx = mp.get_context("fork")  # (the oracle index is inherited; the child touches no GPU)
+    with ctx.Pool(min(len(heavy), 8)) as pool:
+        res = [pool.apply_async(_orc_one, ((reads[r], strat_i, cap),)) for r in heavy]
+        for r, h in zip(heavy, res):
+            try:
+                secs, err, stt = h.get(timeout=400)
+                say("oracle read %d (GPU tier %d): %.1fs %s" % (r, c[r, 12], secs, err or
+                    "states %d fm %d sw %d max queue %d" % stt))
+            except mp.TimeoutError:
+                say("oracle read %d (GPU tier %d): not finished in 400 s" % (r, c[r, 12]))
+        pool.terminate()
+    if ok and len(deep):
         t2 = time.time()
-        s, stt = oi.align([reads[r]], cfg, with_stats=True)
-        say("oracle read %d: %.2fs states %d fm %d (gpu states %d fm %d tier %d)" % (
-            r, time.time() - t2, stt[0].states, stt[0].fm_searches, c[r, 5], c[r, 1], c[r, 12]))
-    t2 = time.time()
-    exp = oi.align([reads[i] for i in deep], cfg, threads=16)
-    say("oracle on %d deep reads %.1fs, identical: %s" % (len(deep), time.time() - t2, exp == got))
-    if exp != got:
-        g, e = got.splitlines(), exp.splitlines()
-        say("first diffs:", [(a, bb) for a, bb in zip(g, e) if a != bb][:3])
+        exp = _ORC["oi"].align([reads[i] for i in deep], O.OrcConfig.default(k=5.0, strategy=strat_i), threads=16)
+        say("oracle on %d deep reads %.1fs, identical: %s" % (len(deep), time.time() - t2, exp == got))
 
 
 if __name__ == "__main__":
