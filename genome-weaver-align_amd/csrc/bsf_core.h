@@ -689,9 +689,9 @@ struct BsfLane {
     const int kk = minMismatches;
     if (row >= kk + 1) return 0;
     const int km = st.kmax;
-    if ((stairBad >> (kk & 63)) & 1) { status = ST_ERROR; return 0; }  // (never reached: stairOk runs first)
+    // (a length whose filter throws never gets here: stairOk ran at the reference's call site)
     if (offset < -km || offset > m) return stairMaskRaw(kk, row, offset);
-    const size_t i = (size_t)(kk * (km + 1) + row) * (size_t)(m + km + 1) + (size_t)(offset + km);
+    const uint32_t i = (uint32_t)((kk * (km + 1) + row) * (m + km + 1) + offset + km);  // (tables < 2^32 words)
     if (stairInLds) return (int64_t)stairLds[i];
     return (int64_t)stairTab[i];
   }

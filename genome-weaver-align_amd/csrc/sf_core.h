@@ -300,10 +300,18 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     const int r = B::alignBlockDetailed(strand, 0, m, refStart, refEnd, &pos, &diff, &co, &cl);
     if (r < 0) return false;
     if (r == 1) return true;  // alignment == null
+    // a dropped hit's CIGAR ops are released (the lane's CIGAR area then holds the listed hits' ops
+    // only: reads on repeats verify millions of candidates)
     int32_t chr, p;
-    if (B::translate(refStart + pos + 1, &chr, &p) != 0) return true;  // UTGBException is logged
+    if (B::translate(refStart + pos + 1, &chr, &p) != 0) {  // UTGBException is logged
+      B::nCigar = co;
+      return true;
+    }
     // reportResult (:345-353): total match length m; a hit above minMismatches is dropped
-    if (m == 0 || diff > minMismatches) return true;
+    if (m == 0 || diff > minMismatches) {
+      B::nCigar = co;
+      return true;
+    }
     const int h = B::newHit(chr, p, m, 0, m, diff, strand, co, cl, 1);
     if (h < 0) return false;
     sfResultAdd(h, diff);
