@@ -1083,7 +1083,9 @@ int gwa_batch_run(gwa_batch_t *b) {
         if (bits & OV_HITS) gHits += 2;
         if (bits & OV_LIST) gList += 2;
         if (bits & OV_CIGAR) gCigar += 2;
-        if (bits & OV_CAND) gCand += 2;
+        // the candidate set straight to >= 2^20 slots (8 MiB per read; half may fill): the reads that
+        // outgrow 16384 candidates on repeats verify hundreds of thousands
+        if (bits & OV_CAND) gCand = std::max(gCand + 2, 6);
         if (!(bits & (OV_ARENA | OV_HEAP | OV_HITS | OV_LIST | OV_CIGAR | OV_CAND)) && !refused)
           throw std::runtime_error(std::to_string(n) + " reads exceeded the largest search tier (overflow bits " +
                                    std::to_string(bits) + ")");
