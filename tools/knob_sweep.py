@@ -2,6 +2,7 @@
 
   python tools/knob_sweep.py --genome hg19 --reads 10000000 --var GWA_WAITQ16 8 12 16
 Prints one line per value: quickscan / search ms (HIP events, mean of --steps after one warmup).
+A value "A=1;B=2" (with --var multi) sets several variables at once; "-" unsets.
 """
 import argparse
 import os
@@ -40,11 +41,20 @@ def main():
     name_blob, name_off = synth.name_blob(a.reads)
     qual_blob = b"I" * (m * a.reads)
     ref = None
+    touched = set()
     for v in a.values:
-        if v == "-":
+        for t in touched:
+            os.environ.pop(t, None)
+        if "=" in v:
+            for kv in v.split(";"):
+                k_, v_ = kv.split("=", 1)
+                os.environ[k_] = v_
+                touched.add(k_)
+        elif v == "-":
             os.environ.pop(a.var, None)  # "-" = unset
         else:
             os.environ[a.var] = v
+            touched.add(a.var)
         b = gwa.Batch(gi, gwa.AlignmentConfig(k=a.k, strategy=a.strategy), blobs=(name_blob, name_off, seq_blob, seq_off, qual_blob, seq_off))
         b.run()
         q = s = 0.0
