@@ -40,6 +40,13 @@ GWA_HD bool anyLane(bool c) {
   return c;
 #endif
 }
+#if defined(GWA_VERIFY_LOG) && !defined(__HIP_DEVICE_COMPILE__)
+// host test builds only: one line per DP verification, to the file $GWA_VERIFY_LOG
+inline FILE *gwaVerifyLog() {
+  static FILE *f = getenv("GWA_VERIFY_LOG") ? fopen(getenv("GWA_VERIFY_LOG"), "w") : nullptr;
+  return f;
+}
+#endif
 // Region timers of the search loop (profiling builds only, -DGWA_PROF): the delta of the
 // shader clock across a region is charged once per wavefront (first active lane), so summing over
 // lanes gives wavefront cycles spent per region.
@@ -1365,6 +1372,9 @@ struct BsfLane {
     const int N = (int)(refEnd - refStart);
     ++numSW;
     verifyBytes += (2 * N + 7) / 8 + (N + 7) / 8 + 32 * bMax;
+#if defined(GWA_VERIFY_LOG) && !defined(__HIP_DEVICE_COMPILE__)
+    if (FILE *vf = gwaVerifyLog()) { fprintf(vf, "V %d %d %d %d %lld %lld\n", caps.hits, strand, qs, qe, (long long)refStart, (long long)refEnd); fflush(vf); }
+#endif
     if (bMax > DB || (size_t)2 * bMax * (N + 1) > (size_t)caps.dpWords) { ovf(OV_DP); return -1; }
     uint64_t pA[DB], pC[DB], pG[DB], pT[DB];
 #pragma unroll
@@ -1633,6 +1643,38 @@ struct BsfLane {
     int64_t refStart = x - k > 0 ? x - k : 0;
     int64_t refEnd = x + frag + k < (int64_t)ix.N ? x + frag + k : (int64_t)ix.N;
     if (refStart > refEnd) { status = ST_ERROR; return -2; }  // IllegalArgumentException in subString
+    // Verification memo (caps.cand > 0: the k >= 4 kernels).  The DP's result -- position, edit
+    // count, CIGAR -- is a function of (strand, query fragment, reference window) alone, and a read
+    // with indels verifies the same window again and again through different split chains (C4: 37 %
+    // of the verifications repeat one of the same read).  A hit made from an unclamped window keeps
+    // refStart + 1 in its pad word, and a small direct-mapped table of the lane's slice points at
+    // the newest such hit per slot; a repeat copies that hit (sharing its CIGAR ops, which are never
+    // changed once written) instead of running the DP again.  Stale slots from earlier reads are
+    // harmless: a slot counts only if its hit index is below nHits and the hit's key matches, and
+    // then it IS this read's result for that window.  numSW / verifyBytes count every call, as the
+    // reference runs the DP every time.
+    const bool memo = caps.cand > 0 && refStart > 0 && refEnd < (int64_t)ix.N;
+    const uint32_t mkey = (uint32_t)refStart + 1u;
+    uint32_t mslot = 0;
+    if (memo) {
+      mslot = ((mkey * 0x9E3779B1u) ^ ((uint32_t)d.start * 0x85EBCA6Bu) ^ ((uint32_t)d.end << 7) ^ (uint32_t)strand) &
+              (uint32_t)(caps.cand - 1);
+      const int hi = (int)(uint32_t)L.cand()[mslot] - 1;
+      if (hi >= 0 && hi < nHits) {
+        const DHit hh = L.hits()[hi];
+        if ((uint32_t)hh.pad == mkey && hh.strand == strand && hh.qStart == (int)d.start && hh.qEnd == (int)d.end) {
+          const int N = (int)(refEnd - refStart), mq = (int)d.end - (int)d.start;
+          const int bMax = mq + 63 >= 64 ? (mq + 63) / 64 : 1;
+          ++numSW;
+          verifyBytes += (2 * N + 7) / 8 + (N + 7) / 8 + 32 * bMax;
+          const int h = newHit(hh.chr, hh.pos, frag, d.start, d.end, hh.diff, strand, hh.cigarOff, hh.cigarLen,
+                               (int)(d.curUb - d.curLb));
+          if (h < 0) return -2;
+          L.hits()[h].pad = (int32_t)mkey;
+          return h;
+        }
+      }
+    }
     int pos = 0, diff = 0, co = 0, cl = 0;
     GWA_PT(tv);
     GWA_PC(PR_NVW, PR_NVL);
@@ -1647,7 +1689,12 @@ struct BsfLane {
     int32_t chr, p;
     if (translate(refStart + pos + 1, &chr, &p) != 0) return -1;
     int h = newHit(chr, p, frag, d.start, d.end, diff, strand, co, cl, (int)(d.curUb - d.curLb));
-    return h < 0 ? -2 : h;
+    if (h < 0) return -2;
+    if (memo) {
+      L.hits()[h].pad = (int32_t)mkey;
+      L.cand()[mslot] = (int64_t)(h + 1);
+    }
+    return h;
   }
 
   // reportAlignment (:562-586); returns false on overflow/error

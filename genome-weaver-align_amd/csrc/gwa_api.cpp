@@ -904,9 +904,9 @@ int gwa_batch_run(gwa_batch_t *b) {
     int arenaMaxLog = 24;
     if (const char *e = getenv("GWA_MAX_STATES_LOG2"))  // diagnostics (tools/diag_sf.py): a lower state limit
       arenaMaxLog = std::max(16, std::min(24, atoi(e)));
-    while (n > 0) {
-      if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
-      const int tb = std::min(t, kNumTiers - 1);  // t > kNumTiers - 1: the last tier, grown
+    const bool hybrid = !sf && b->R >= 8;
+    // the capacities of tier tb (the last one grown by the g* shifts)
+    auto capsFor = [&](int tb) {
       const Tier &T = sf ? kSfTiers[tb] : kTiers[tb];
       Caps caps;
       caps.sparse = 0;
@@ -914,10 +914,15 @@ int gwa_batch_run(gwa_batch_t *b) {
       // GWA_TIER_ARENA="a0,a1,a2,a3": arena / heap states of tiers >= 1, and of tier 0 for the
       // hybrid-heap (k >= 4) kernels, whose heap is not bounded by the LDS array (tuning runs)
       if ((tb > 0 || b->R >= 8) && !sf) {
+        // k >= 4: hit lists of 128 / 256 entries in tiers 0 / 1 (C4: 32 / 64 sent 241k / 108k of 833k
+        // reads to a rerun, 128 / 256 151k / 5k; search 457 -> 409 ms per 1M reads)
+        const bool wide = b->R >= 8 && tb < 2;
+        const uint32_t dh = wide ? (tb == 0 ? 128u : 256u) : (uint32_t)T.hits;
+        const uint32_t dc = wide ? (tb == 0 ? 2048u : 4096u) : (uint32_t)T.cigar;
         const int a = (int)std::min<uint32_t>(tierValue("GWA_TIER_ARENA", tb, (uint32_t)T.arena), 1u << 24);
         caps.arena = caps.heap = a;
-        caps.hits = caps.list = (int)tierValue("GWA_TIER_HITS", tb, (uint32_t)T.hits);  // hit list / report list
-        caps.cigar = (int)tierValue("GWA_TIER_CIGAR", tb, (uint32_t)T.cigar);
+        caps.hits = caps.list = (int)tierValue("GWA_TIER_HITS", tb, dh);  // hit list / report list
+        caps.cigar = (int)tierValue("GWA_TIER_CIGAR", tb, dc);
       }
       caps.cand = T.cand;
       caps.sf = sf ? 1 : 0;
@@ -929,17 +934,48 @@ int gwa_batch_run(gwa_batch_t *b) {
         caps.cigar <<= gCigar;
         caps.cand <<= gCand;
       }
+      // -m bsf, k >= 4 (R >= 8): the verification memo (bsf_core.h verify), twice the hit list's
+      // entries, a power of two; k <= 3 reads do not repeat verifications (C2: 1431 of 1431 unique)
+      // and skip the lookup.  GWA_VERIFY_MEMO=0 turns it off (A/B runs).
+      if (!sf) {
+        caps.cand = 0;
+        const char *vm = getenv("GWA_VERIFY_MEMO");
+        if (b->R >= 8 && !(vm && atoi(vm) == 0)) {
+          int c = 64;
+          while (c < 2 * caps.hits && c < (1 << 22)) c <<= 1;
+          caps.cand = c;
+        }
+      }
       // k >= 4 (R >= 8): a hybrid heap, its top slots in LDS and the rest in the slice, holding as
       // many entries as the arena has states (k >= 4 heaps outgrow the 8-slot LDS heap of tier 0)
-      const bool hybrid = !sf && b->R >= 8;
       if (hybrid) caps.heap = caps.arena;
       const int bMax = std::max(1, (m + 63) / 64);
       const int nref = m + 2 * b->kmax + 2;
       caps.dpWords = 2 * bMax * (nref + 1);
       caps.path = m + nref + 8;
       caps.dpSlice = tb == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
-      const uint64_t stride = laneBytesFor(b->R, caps), ilv = ilvBytesFor(caps);
+      return caps;
+    };
+    while (n > 0) {
+      if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
       const uint64_t budget = scratchBudget(ix);
+      // Few reads left after the first tier: straight to the largest tier whose capacities give every
+      // one of them a slice within the scratch budget.  A rerun restarts a search from its seeds, and
+      // the reads still overflowing here are the heaviest (C4 -m bsf: 5k reads in tier 2, of which 2
+      // then reran on tier 3 for 65 ms).  GWA_TIER_JUMP=0 turns it off.
+      if (t >= 1 && t < kNumTiers - 1 && !(getenv("GWA_TIER_JUMP") && atoi(getenv("GWA_TIER_JUMP")) == 0)) {
+        for (int u = kNumTiers - 1; u > t; --u) {
+          const Caps lc = capsFor(u);
+          if ((uint64_t)n * (laneBytesFor(b->R, lc) + ilvBytesFor(lc)) <= budget) {
+            t = u;
+            break;
+          }
+        }
+      }
+      const int tb = std::min(t, kNumTiers - 1);  // t > kNumTiers - 1: the last tier, grown
+      const Tier &T = sf ? kSfTiers[tb] : kTiers[tb];
+      Caps caps = capsFor(tb);
+      const uint64_t stride = laneBytesFor(b->R, caps), ilv = ilvBytesFor(caps);
       const uint64_t maxSparse = tierValue("GWA_SPARSE_LANES", 0, 262144u);
       // scratch of `ln` lanes of which every sp-th takes reads: slices for the active ones, the
       // interleaved DP block for all (bsf_search_kernel / sf_search_kernel addressing)

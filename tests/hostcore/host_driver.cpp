@@ -34,7 +34,10 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
   // overflows into the next tier): the slice fallback path gives the same SAM
   const int sl = 1 + (getenv("GWA_TEST_SLICE_SHIFT") ? atoi(getenv("GWA_TEST_SLICE_SHIFT")) : 0);
   // (k >= 4, R >= 8: the GPU's hybrid heap holds as many entries as the arena, gwa_batch_run)
-  const Caps tiers[4] = {{256, R >= 8 ? 256 : kLdsHeap, 32, 32, 512, dpw, path, sl, 0}, {1024, 1024, 64, 64, 1024, dpw, path, 0, 0},
+  // (k >= 4: hit lists of 128 / 256 in tiers 0 / 1, gwa_batch_run)
+  const bool w = R >= 8;
+  const Caps tiers[4] = {{256, w ? 256 : kLdsHeap, w ? 128 : 32, w ? 128 : 32, w ? 2048 : 512, dpw, path, sl, 0},
+                         {1024, 1024, w ? 256 : 64, w ? 256 : 64, w ? 4096 : 1024, dpw, path, 0, 0},
                          {4096, 4096, 256, 256, 4096, dpw, path, 0, 0}, {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 0}};
   // -m sf tiers (gwa_api.cpp kSfTiers)
   const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, sl, 32, 0, 1}, {2048, 2048, 64, 64, 2048, dpw, path, 0, 256, 0, 1},
@@ -64,11 +67,22 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
     // exceeded ones; doubling all of them gives the same results, capacities only decide overflow)
     for (int t = 0; t < 14; ++t) {
       Caps sc = sfTiers[t < 4 ? t : 3], bc = tiers[t < 4 ? t : 3];
+      if (t == 0 && getenv("HC_T0_HITS")) { bc.hits = bc.list = atoi(getenv("HC_T0_HITS")); bc.cigar = 16 * bc.hits; }  // experiments
+      if (t == 1 && getenv("HC_T1_HITS")) { bc.hits = bc.list = atoi(getenv("HC_T1_HITS")); bc.cigar = 16 * bc.hits; }
+      if (t == 0 && getenv("HC_T0_ARENA")) { bc.arena = bc.heap = atoi(getenv("HC_T0_ARENA")); }
       if (t >= 4) {
         const int g = t - 3;
         for (Caps *c : {&sc, &bc}) {
           c->arena <<= g; c->heap <<= g; c->hits <<= g; c->list <<= g; c->cigar <<= g; c->cand <<= g;
         }
+      }
+      // the k >= 4 verification memo, as gwa_batch_run sizes it (GWA_VERIFY_MEMO=0: off)
+      bc.cand = 0;
+      if (R >= 8 && !(getenv("GWA_VERIFY_MEMO") && atoi(getenv("GWA_VERIFY_MEMO")) == 0)) {
+        bc.cand = 64;
+        while (bc.cand < 2 * bc.hits && bc.cand < (1 << 22)) bc.cand <<= 1;
+      }
+      {
         const size_t need = std::max(laneBytes<R>(sc), laneBytes<R>(bc)) + ilvBytes(bc) + 4096;
         if (scratch.size() < need) scratch.resize(need);
       }
@@ -99,6 +113,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         lane.writeSearchOutput(&hd, os, 0);
       }
       if (traced) tv[0] = (uint32_t)lane.traceN;
+      if (hd.status == ST_OVERFLOW && getenv("HC_OVF_LOG")) fprintf(stderr, "[hc] read %u tier %d overflow 0x%x\n", i, t, hd.ovfWhat);
       if (hd.status != ST_OVERFLOW) break;
     }
     if (traced) {
