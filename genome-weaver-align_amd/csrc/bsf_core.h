@@ -677,9 +677,15 @@ struct BsfLane {
   // getStairCaseMask64bit from the mask words behind the table (offsets outside [-kmax, m]):
   // offset >= 0: (~0L << (m - offset)) | mask.substring64(offset, offset + 64), else
   // mask.substring64(0, 64) << -offset (S/StaircaseFilter.java:91-102, A/BitVector.java:106-116)
-  GWA_HD int64_t stairMaskRaw(int kk, int row, int offset) const {
-    const int km = st.kmax, W = (m + 63) / 64;
-    const uint64_t *v = stairTab + (size_t)(km + 2) * (km + 1) * (size_t)(m + km + 1) + (size_t)(kk * (km + 1) + row) * W;
+  // (a static function of plain values, not inlined for R >= 8: the path is rare -- reads whose
+  // (byte) chunk starts wrap, > ~223 bp -- and inlined into the automaton step's unrolled rows it
+  // cost the R = 8 kernels 40-45 spilled VGPRs; the R = 4 kernels spill more with the call)
+  GWA_HDNI static int64_t stairMaskRawNI(const uint64_t *tab, int km, int m, int kk, int row, int offset) {
+    return stairMaskRaw(tab, km, m, kk, row, offset);
+  }
+  GWA_HD static int64_t stairMaskRaw(const uint64_t *tab, int km, int m, int kk, int row, int offset) {
+    const int W = (m + 63) / 64;
+    const uint64_t *v = tab + (size_t)(km + 2) * (km + 1) * (size_t)(m + km + 1) + (size_t)(kk * (km + 1) + row) * W;
     auto sub64 = [&](int64_t start, int64_t end) -> int64_t {  // start >= 0
       const int pos = (int)(start / 64);
       if (pos >= W) return 0;
@@ -692,12 +698,19 @@ struct BsfLane {
     if (offset >= 0) return jshl(~0LL, m - offset) | sub64(offset, (int64_t)offset + 64);
     return jshl(sub64(0, 64), -offset);
   }
+  // WRAP: offsets outside the table are possible -- -m sf reads whose (byte) chunk starts wrap (a
+  // negative SFState offset); the BSF automaton's offsets (processed bases - rows) never leave it
+  template <bool WRAP>
   GWA_HD int64_t stairMask(int row, int offset) {
     const int kk = minMismatches;
     if (row >= kk + 1) return 0;
     const int km = st.kmax;
     // (a length whose filter throws never gets here: stairOk ran at the reference's call site)
-    if (offset < -km || offset > m) return stairMaskRaw(kk, row, offset);
+#if !defined(__HIP_DEVICE_COMPILE__)
+    if (!WRAP && (offset < -km || offset > m)) abort();  // host builds check the claim above
+#endif
+    if (WRAP && (offset < -km || offset > m))
+      return R >= 8 ? stairMaskRawNI(stairTab, km, m, kk, row, offset) : stairMaskRaw(stairTab, km, m, kk, row, offset);
     const uint32_t i = (uint32_t)((kk * (km + 1) + row) * (m + km + 1) + offset + km);  // (tables < 2^32 words)
     if (stairInLds) return (int64_t)stairLds[i];
     return (int64_t)stairTab[i];
@@ -1731,6 +1744,7 @@ struct BsfLane {
     return nfaCore(s.nfa, height, kOff, qeq, cProcessed(s), cFrag(s), outRows, outH, outKOff, hasMatch);
   }
   // ReadAlignmentNFA.nextState(qeq, progressIndex, fragmentLength, ...) (S/ReadAlignmentNFA.java:146-203)
+  template <bool WRAP = false>
   GWA_HD bool nfaCore(const uint64_t (&nfa)[R], int height, int kOff, int64_t qeq, int progress, int frag,
                       uint64_t (&outRows)[R], int *outH, int *outKOff, bool *hasMatch) {
     const int kk = kOff + height - 1;
@@ -1747,11 +1761,11 @@ struct BsfLane {
         int64_t nx = jshl(a & qeq, 1);
         if (i == 0) {
           if (nx != 0) { minKwithMatch = 0; minKwithProgress = 0; }
-          nx &= stairMask(kOff, soff);
+          nx &= stairMask<WRAP>(kOff, soff);
         } else {
           if (minKwithMatch > kk && nx != 0) minKwithMatch = i;
           nx |= prevRow | jshl(prevRow, 1) | jshl(prevNext, 1);
-          nx &= stairMask(kOff + i, soff);
+          nx &= stairMask<WRAP>(kOff + i, soff);
           if (minKwithProgress > kk && (nx & jshl(1, height)) != 0) minKwithProgress = i;
         }
         next[i] = nx;
@@ -2128,13 +2142,15 @@ struct BsfLane {
       // children (:386-410): nextBase first -- a state from it ends the iteration -- then every
       // base still unchecked; one FM step per call
       GWA_PT(te);
+      // (the checked flags are stored once, with the child taken below or with the split flag: nothing
+      // reads the arena copy of xC in between, siIsEmpty reads the register copy)
       int ch = -1, tt = xT, zero = 0;
       for (; tt < 4 && ch < 0; ++tt) {
         zero |= tt == 0 ? 1 : 0;  // (single-exit loop, integer state: see quickScan)
         const int cand = tt < 0 ? xNextBase : tt;
         if (xCS.state & (1 << cand)) continue;  // isChecked
         xCS.state |= 1 << cand;                 // updateFlag
-        if (siIsEmpty(xCS, cand)) { storeStateWord(xC, xCS.state); continue; }
+        if (siIsEmpty(xCS, cand)) continue;
         ch = cand;
       }
       // StaircaseFilter sf = getStairCaseFilter(m) where the loop over every base begins (:439); this

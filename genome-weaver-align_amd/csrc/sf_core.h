@@ -59,8 +59,16 @@ struct SfLane : BsfLane<R, QW, false, 24> {
   // A polled SFState is never read again (the loop works on its register copy; SF has no split
   // chains), so its arena slot is recycled: the arena holds the queued states only, and its size
   // bounds the live queue, not the states created.  Free slots are linked through SfState::lb.
-  int freeHead = -1, created = 0;
+  // The newest free slot is kept in a register (spare): a step frees the polled state and then
+  // allocates its children, and taking the spare costs no memory round trip, where popping the list
+  // waits on a load of the link.
+  int freeHead = -1, spare = -1, created = 0;
   GWA_HD int sfAlloc() {
+    if (spare >= 0) {
+      const int id = spare;
+      spare = -1;
+      return id;
+    }
     if (freeHead >= 0) {
       const int id = freeHead;
       freeHead = (int)arena()[id].lb;
@@ -69,8 +77,11 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     return B::allocState();
   }
   GWA_HD void sfFree(int id) {
-    arena()[id].lb = (uint32_t)freeHead;
-    freeHead = id;
+    if (spare >= 0) {
+      arena()[spare].lb = (uint32_t)freeHead;
+      freeHead = spare;
+    }
+    spare = id;
   }
 
   // candidates[strand].contains(start) / add: a linear scan of L.cand() for the small sets of the
@@ -328,7 +339,7 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     uint64_t rows[R];
     int nh = 0, nko = 0;
     bool hm = false;
-    if (!B::nfaCore(c.nfa, c.nrows, c.kOffset, qeq, nextIndex - c.offset, m - c.offset, rows, &nh, &nko, &hm))
+    if (!B::template nfaCore<true>(c.nfa, c.nrows, c.kOffset, qeq, nextIndex - c.offset, m - c.offset, rows, &nh, &nko, &hm))
       return true;  // null: numFiltered++
     const int diff = nko - c.kOffset;
     int newScore = c.score - diff * cfg.mismatchPenalty;
@@ -362,7 +373,7 @@ struct SfLane : BsfLane<R, QW, false, 24> {
 
   GWA_HD void sfSearch() {
     candClear();
-    freeHead = -1;
+    freeHead = spare = -1;
     created = 0;
     if (!sfStart()) return;
     while (sfStep()) {

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--genome", default="hg19")
     ap.add_argument("--reads", type=int, default=0)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--strategy", default="bsf")
     ap.add_argument("--env", action="append", default=[], help="per-variant env: IDX:VAR=VAL (applied around its calls)")
     args = ap.parse_args()
     import numpy as np
@@ -66,7 +67,7 @@ def main():
         gi = g.FMIndexOnGenome.buildFromCodes(codes, names, lengths)
         for k, v in envs.get(i, {}).items():
             os.environ[k] = v
-        b = g.Batch(gi, g.AlignmentConfig(k=5.0 if c4 else 2.0), blobs=blobs)
+        b = g.Batch(gi, g.AlignmentConfig(k=5.0 if c4 else 2.0, strategy=args.strategy), blobs=blobs)
         for k in envs.get(i, {}):
             del os.environ[k]
         vs.append((p, g, gi, b))
