@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "bsf_core.h"
+#include "sf_core.h"
 #include "host_index.h"
 #include "kernels.h"
 #include "sam.h"
@@ -93,6 +94,7 @@ struct gwa_batch {
   uint32_t n = 0;
   bool hasQual = false;
   int maxM = 0, kmax = 0, R = 4;
+  bool sfWrap = false;  // some read's -m sf prefix-scan chunks wrap (sfChunksWrap): the WRAP kernel instance
   // the read text in HBM: bases (encoded on the device into d_codes), names and qualities (read by
   // the SAM writer).  Read r's bases are d_seqText[d_seqB[r], d_seqE[r]) etc.: SoA blobs (E = B + 1)
   // or, from the pipeline, the fields of FASTQ records inside one copy of the file text.
@@ -574,9 +576,11 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
     throw std::runtime_error("read longer than " + std::to_string(kMaxReadLen) + " bp in this batch (" +
                              std::to_string(b->maxM) + " bp): the device path aligns reads of at most " +
                              std::to_string(kMaxReadLen) + " bp");
+  b->sfWrap = false;
   for (int m : lens) {
     int k = (cfg->k > 0 && cfg->k < 1) ? (int)floor((double)((float)m * cfg->k)) : (int)cfg->k;
     b->kmax = std::max(b->kmax, k);
+    if (m > 0 && k >= 0 && k <= 31 && sfChunksWrap(m, k + 1)) b->sfWrap = true;  // -m sf kernel instance
   }
   if (b->kmax > 31) throw std::runtime_error("k > 31 is not supported on the device path");
   {  // the queue keys hold score() in 24 bits (BsfLane::packKey): |score| < 2^23 for these scores
@@ -1053,7 +1057,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       }
 #else
       if (sf)
-        launchSfSearch(b->R, qwFor(b->maxM), lanes, ix->view, b->scfg, b->st, rv,
+        launchSfSearch(b->R, qwFor(b->maxM), b->sfWrap, lanes, ix->view, b->scfg, b->st, rv,
                        (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s);
       else

@@ -316,17 +316,17 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
                    ovfList, ovfCount, ovfBits, s, trace, traceRead);
 }
 
-void launchSfSearch(int R, int QW, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+void launchSfSearch(int R, int QW, bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                     const Caps &caps, OutHeader *oh, const OutSlots &os,
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
                     hipStream_t s) {
   if (n == 0) return;
   if (QW == 4)
-    launchSfSearchT<4>(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
+    launchSfSearchT<4>(R, false, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
                        ovfCount, ovfBits, s);
   else if (QW == 8)
-    launchSfSearchT<8>(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
+    launchSfSearchT<8>(R, wrap, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
                        ovfCount, ovfBits, s);
   else
     launchSfSearch16(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,

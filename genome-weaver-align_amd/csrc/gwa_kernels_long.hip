@@ -24,7 +24,7 @@ void launchSfSearch16(int R, uint32_t lanes, const IndexView &ix, const SearchCo
                       const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                       const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
                       uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s) {
-  launchSfSearchT<16>(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
+  launchSfSearchT<16>(R, true, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
                       ovfCount, ovfBits, s);
 }
 

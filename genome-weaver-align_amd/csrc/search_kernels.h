@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 
 // sf_search<R, QW>: persistent lanes over the read list, one read per lane per iteration (lanes take
 // reads from a shared counter, one atomic per wavefront); overflowing reads go to the next tier.
-template <int R, int QW>
+template <int R, int QW, bool WRAP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES)))
 sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
                  uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
@@ -235,7 +235,7 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
     __syncthreads();
   }
   __shared__ uint64_t qwLds[2 * QW * 256];
-  SfLane<R, QW> lane(ix, cfg, st, L, caps);
+  SfLane<R, QW, WRAP> lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
   if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
   lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
@@ -317,22 +317,27 @@ void launchSearchT(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, cons
   }
 }
 
+// wrap: the batch has reads whose prefix-scan chunks wrap (sfChunksWrap); QW = 4 reads (<= 128 bp)
+// never do, QW = 16 reads are always run with the WRAP path
 template <int QW>
-void launchSfSearchT(int R, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+void launchSfSearchT(int R, bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                      const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                      const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
                      uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s) {
   dim3 grid((lanes + 255) / 256);
-  switch (R) {
-#define GWA_SF(RR)                                                                                                     \
-  case RR:                                                                                                             \
-    hipLaunchKernelGGL((sf_search_kernel<RR, QW>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,        \
-                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);                           \
+  constexpr bool kNever = QW == 4, kAlways = QW == 16;
+  const int key = R * 2 + ((kAlways || (wrap && !kNever)) ? 1 : 0);
+  switch (key) {
+#define GWA_SF(RR, WW)                                                                                                 \
+  case RR * 2 + WW:                                                                                                    \
+    if (!(WW ? kNever : kAlways))                                                                                      \
+      hipLaunchKernelGGL((sf_search_kernel<RR, QW, WW ? !kNever : kAlways>), grid, dim3(256), 0, s, ix, cfg, st, reads, \
+                         list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);      \
     break;
-    GWA_SF(4)
-    GWA_SF(8)
-    GWA_SF(16)
-    GWA_SF(32)
+    GWA_SF(4, 0) GWA_SF(4, 1)
+    GWA_SF(8, 0) GWA_SF(8, 1)
+    GWA_SF(16, 0) GWA_SF(16, 1)
+    GWA_SF(32, 0) GWA_SF(32, 1)
 #undef GWA_SF
     default: break;
   }

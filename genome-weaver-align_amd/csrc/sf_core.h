@@ -28,7 +28,32 @@ struct SfState {
 static_assert(sizeof(SfState<4>) == 24 + 8 * 4 && sizeof(SfState<8>) == 24 + 8 * 8 && sizeof(SfState<32>) == 24 + 8 * 32,
               "SfState size must match stateBytes (bsf_core.h)");
 
-template <int R, int QW>
+// StaircaseFilter(m, kk) chunk i with the reference's (byte) arithmetic (S/StaircaseFilter.java:47-67);
+// kk >= 1 here (the prefix scan runs at minMismatches = k + 1)
+GWA_HD void sfChunk(int m_, int kk, int i, int *start, int *len) {
+  const int lastChunkSize = (m_ - kk >= 6) ? m_ * 2 / (kk + 2) : m_ - kk;
+  const int rest = (int)(int8_t)(uint8_t)(m_ - lastChunkSize);
+  const int s0 = (int)(int8_t)(uint8_t)(rest * i / kk);
+  const int s1 = i + 1 <= kk ? (int)(int8_t)(uint8_t)(rest * (i + 1) / kk) : (int)(int8_t)(uint8_t)m_;
+  *start = s0;
+  *len = (int)(int8_t)(uint8_t)(s1 - s0);
+}
+// true when some prefix-scan chunk of an m-base read at minMismatches kk starts outside [0, m] or
+// ends past m: only then can an SFState offset leave the staircase table's range (the automaton's
+// masks then come from SfLane's WRAP path); the host picks the kernel instance from this
+GWA_HD bool sfChunksWrap(int m_, int kk) {
+  int wrap = 0;
+  for (int c = 0; c <= kk; ++c) {
+    int cs = 0, w = 0;
+    sfChunk(m_, kk, c, &cs, &w);
+    wrap |= (cs < 0 || cs > m_ || cs + (w > 0 ? w : 0) > m_) ? 1 : 0;
+  }
+  return wrap != 0;
+}
+
+// WRAP: the batch has reads whose chunk starts wrap (sfChunksWrap); without them the automaton's
+// out-of-table mask path is compiled out (it cost the R = 8 kernel ~35 spilled VGPRs)
+template <int R, int QW, bool WRAP = true>
 struct SfLane : BsfLane<R, QW, false, 24> {
   typedef BsfLane<R, QW, false, 24> B;
   using B::ix;
@@ -141,16 +166,7 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     return id;
   }
 
-  // StaircaseFilter(m, kk) chunk i with the reference's (byte) arithmetic (S/StaircaseFilter.java:47-67);
-  // kk >= 1 here (the prefix scan runs at minMismatches = k + 1)
-  GWA_HD static void chunk(int m_, int kk, int i, int *start, int *len) {
-    const int lastChunkSize = (m_ - kk >= 6) ? m_ * 2 / (kk + 2) : m_ - kk;
-    const int rest = (int)(int8_t)(uint8_t)(m_ - lastChunkSize);
-    const int s0 = (int)(int8_t)(uint8_t)(rest * i / kk);
-    const int s1 = i + 1 <= kk ? (int)(int8_t)(uint8_t)(rest * (i + 1) / kk) : (int)(int8_t)(uint8_t)m_;
-    *start = s0;
-    *len = (int)(int8_t)(uint8_t)(s1 - s0);
-  }
+  GWA_HD static void chunk(int m_, int kk, int i, int *start, int *len) { sfChunk(m_, kk, i, start, len); }
 
   // PrefixScan.scanRead for one chunk: exact forward search of q[strand][cs, cs + w) from [0, N).
   // Returns 0 = mismatch (null si), 1 = rows [lb, ub), 2 = one row whose SA value is *lb.
@@ -339,7 +355,7 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     uint64_t rows[R];
     int nh = 0, nko = 0;
     bool hm = false;
-    if (!B::template nfaCore<true>(c.nfa, c.nrows, c.kOffset, qeq, nextIndex - c.offset, m - c.offset, rows, &nh, &nko, &hm))
+    if (!B::template nfaCore<WRAP>(c.nfa, c.nrows, c.kOffset, qeq, nextIndex - c.offset, m - c.offset, rows, &nh, &nko, &hm))
       return true;  // null: numFiltered++
     const int diff = nko - c.kOffset;
     int newScore = c.score - diff * cfg.mismatchPenalty;
