@@ -323,7 +323,7 @@ void launchSfSearch(int R, int QW, bool wrap, uint32_t lanes, const IndexView &i
                     hipStream_t s) {
   if (n == 0) return;
   if (QW == 4)
-    launchSfSearchT<4>(R, false, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
+    launchSfSearchT<4>(R, wrap, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
                        ovfCount, ovfBits, s);
   else if (QW == 8)
     launchSfSearchT<8>(R, wrap, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,

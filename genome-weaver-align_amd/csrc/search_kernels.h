@@ -317,21 +317,21 @@ void launchSearchT(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, cons
   }
 }
 
-// wrap: the batch has reads whose prefix-scan chunks wrap (sfChunksWrap); QW = 4 reads (<= 128 bp)
-// never do, QW = 16 reads are always run with the WRAP path
+// wrap: the batch has reads whose prefix-scan chunks wrap (sfChunksWrap: some lengths of 129-256 bp,
+// and reads of <= 31 bp at a large k); QW = 16 reads are always run with the WRAP path
 template <int QW>
 void launchSfSearchT(int R, bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                      const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                      const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
                      uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s) {
   dim3 grid((lanes + 255) / 256);
-  constexpr bool kNever = QW == 4, kAlways = QW == 16;
-  const int key = R * 2 + ((kAlways || (wrap && !kNever)) ? 1 : 0);
+  constexpr bool kAlways = QW == 16;
+  const int key = R * 2 + ((kAlways || wrap) ? 1 : 0);
   switch (key) {
 #define GWA_SF(RR, WW)                                                                                                 \
   case RR * 2 + WW:                                                                                                    \
-    if (!(WW ? kNever : kAlways))                                                                                      \
-      hipLaunchKernelGGL((sf_search_kernel<RR, QW, WW ? !kNever : kAlways>), grid, dim3(256), 0, s, ix, cfg, st, reads, \
+    if (WW || !kAlways)                                                                                                \
+      hipLaunchKernelGGL((sf_search_kernel<RR, QW, WW ? true : kAlways>), grid, dim3(256), 0, s, ix, cfg, st, reads,   \
                          list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);      \
     break;
     GWA_SF(4, 0) GWA_SF(4, 1)

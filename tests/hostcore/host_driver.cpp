@@ -241,3 +241,6 @@ int hc_align(void *p, float k, int reportType, int numSplit, int strategy, uint3
 
 // the encode kernels' byte-parallel ACGT.to3bitCode (text_core.h)
 extern "C" uint32_t hc_to3bit4(uint32_t x) { return to3bit4(x); }
+
+// the -m sf kernel-instance rule (sf_core.h sfChunksWrap; search_kernels.h launchSfSearchT)
+extern "C" int hc_sf_chunks_wrap(int m, int kk) { return sfChunksWrap(m, kk) ? 1 : 0; }

@@ -255,6 +255,26 @@ def test_sf_edge_reads(random_pair):
     _check(gi, oi, reads, k=2.0, strategy="sf")
 
 
+@pytest.mark.parametrize("k", [6.0, 12.0])
+def test_sf_short_reads_large_k(random_pair, k):
+    """Reads of 8-31 bp at a large k: their prefix-scan chunks wrap or run past the read
+    (sfChunksWrap), so the batch runs the -m sf instance with the wrapped-offset staircase path;
+    compared with the oracle (errors and unmapped reads included), and the same reads with -m bsf."""
+    codes, names, lengths, gi, oi = random_pair
+    rng = np.random.default_rng(int(k) + 40)
+    L = len(codes)
+    reads = []
+    for i in range(400):
+        m = int(rng.integers(8, 32))
+        a = int(rng.integers(0, L - m))
+        s = codes[a:a + m].copy()
+        for j in rng.integers(0, m, rng.integers(0, 3)):
+            s[j] = (s[j] + 1) % 4 if s[j] < 4 else s[j]
+        reads.append(("s%d" % i, synth.SYM[s].tobytes().decode(), None))
+    _check(gi, oi, reads, k=k, strategy="sf")
+    _check(gi, oi, reads, k=k, strategy="bsf")
+
+
 def test_sf_known_answer_queries_on_gpu(gwa):
     # the two SuffixFilterTest queries (T/strategy/SuffixFilterTest.java:67-76) on sample3.fa
     fa = open(os.path.join(HERE, "golden", "fixtures", "sample3.fa")).read()

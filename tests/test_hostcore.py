@@ -290,3 +290,19 @@ def test_long_reads_read_by_read(strategy, m, k):
         errs += e is None
         ok += e is not None
     assert ok > 0
+
+
+def test_sf_wrap_instance_rule():
+    """The -m sf kernel instance without the wrapped-offset staircase path is picked only for batches
+    whose reads' prefix-scan chunks stay inside the read (sfChunksWrap false): the usual lengths
+    (36-150 bp, k <= 10) do; reads of <= 31 bp at a large k and some 129-512 bp lengths do not, and
+    their batches run the WRAP instance (launchSfSearchT)."""
+    import ctypes
+    L = hostcore.lib()
+    L.hc_sf_chunks_wrap.restype = ctypes.c_int
+    L.hc_sf_chunks_wrap.argtypes = [ctypes.c_int, ctypes.c_int]
+    assert not any(L.hc_sf_chunks_wrap(m, k + 1) for m in (36, 50, 100, 128, 150) for k in range(0, 11))
+    wraps = [(m, kk) for m in range(1, 129) for kk in range(1, 33) if L.hc_sf_chunks_wrap(m, kk)]
+    assert wraps and max(m for m, _ in wraps) <= 31
+    assert any(L.hc_sf_chunks_wrap(m, kk) for m in range(129, 257) for kk in range(1, 33))
+    assert any(L.hc_sf_chunks_wrap(m, kk) for m in range(257, 513) for kk in range(1, 33))
