@@ -594,8 +594,9 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   }
   b->R = b->kmax + 1 <= 4 ? 4 : b->kmax + 1 <= 8 ? 8 : b->kmax + 1 <= 16 ? 16 : 32;
   // report-batch threshold: 14/16 for k <= 3 (C2: 14-16 tie, 12 is 2 % slower; hg19r favours 14),
-  // 10/16 for k >= 4 (C4 -m bsf: 8 / 10 / 12 / 14 / 16 -> 447 / 447 / 454 / 489 / 684 ms per 1M reads)
-  if (b->scfg.waitQ16 <= 0) b->scfg.waitQ16 = b->R >= 8 ? 10 : 14;
+  // 8/16 for k >= 4 (C4 -m bsf, round-4 tiers: 6 / 8 / 10 / 12 -> 323-330 / 315-316 / 320-330 / 346 ms
+  // per 1M reads, tier 0 109 ms at 8 against 113-114 at 10)
+  if (b->scfg.waitQ16 <= 0) b->scfg.waitQ16 = b->R >= 8 ? 8 : 14;
   std::vector<uint64_t> tab, bad;
   std::vector<uint32_t> base;
   buildStairTables(lens, std::max(b->kmax, 0), tab, base, bad);
