@@ -1665,7 +1665,8 @@ struct BsfLane {
     // changed once written) instead of running the DP again.  Stale slots from earlier reads are
     // harmless: a slot counts only if its hit index is below nHits and the hit's key matches, and
     // then it IS this read's result for that window.  numSW / verifyBytes count every call, as the
-    // reference runs the DP every time.
+    // reference runs the DP every time.  (The key refStart + 1 is exact: the host refuses texts of
+    // 2^32 - 1 bases or more, gwa_api.cpp checkSize, so refStart + 1 < 2^32.)
     const bool memo = caps.cand > 0 && refStart > 0 && refEnd < (int64_t)ix.N;
     const uint32_t mkey = (uint32_t)refStart + 1u;
     uint32_t mslot = 0;

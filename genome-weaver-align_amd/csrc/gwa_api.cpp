@@ -583,14 +583,17 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
     if (m > 0 && k >= 0 && k <= 31 && sfChunksWrap(m, k + 1)) b->sfWrap = true;  // -m sf kernel instance
   }
   if (b->kmax > 31) throw std::runtime_error("k > 31 is not supported on the device path");
-  {  // the queue keys hold score() in 24 bits (BsfLane::packKey): |score| < 2^23 for these scores
-    const int64_t s = std::max(1, cfg->num_split), T = (s + 1) * s / 2;
+  {  // the -m bsf queue keys hold score() in 24 bits (BsfLane::packKey): |score| < 2^23 for these
+     // scores; the -m sf keys (SfLane::keyOf) hold it in 32 bits and have no split chains
+    const bool sfPath = cfg->strategy == 1;
+    const int64_t s = sfPath ? 0 : std::max(1, cfg->num_split), T = (s + 1) * s / 2;
     const int64_t M = std::llabs((int64_t)cfg->match), Nn = std::llabs((int64_t)cfg->mismatch);
     const int64_t S = std::llabs((int64_t)cfg->split_open);
     const int64_t bound = M * b->maxM + (M + Nn) * (255 * (s + 1) + T) + S * T;
-    if (cfg->num_split > 64 || bound >= (1LL << 23))
+    const int lim = sfPath ? 31 : 23;
+    if ((!sfPath && cfg->num_split > 64) || bound >= (1LL << lim))
       throw std::runtime_error("scoring parameters too large for the device's queue keys (|score| may reach " +
-                               std::to_string(bound) + ", limit 2^23)");
+                               std::to_string(bound) + ", limit 2^" + std::to_string(lim) + ")");
   }
   b->R = b->kmax + 1 <= 4 ? 4 : b->kmax + 1 <= 8 ? 8 : b->kmax + 1 <= 16 ? 16 : 32;
   // report-batch threshold: 14/16 for k <= 3 (C2: 14-16 tie, 12 is 2 % slower; hg19r favours 14),
@@ -882,7 +885,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     const bool sf = b->cfg.strategy == 1;
     if (!sf)
       launchQuickscan(qwFor(b->maxM), ix->view, b->scfg, rv, b->d_sres, b->d_oh, outSlots(b), b->d_list[0],
-                      b->d_count, nullptr, s);
+                      b->d_count, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
     uint32_t nSearch = b->n;
@@ -1161,9 +1164,9 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipGetLastError());
       uint32_t hc[2] = {0, 0};
       HIPCHK(hipMemcpyAsync(hc, heavyCount, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));  // (hc is read only after the copy has landed)
       const uint32_t nHeavy = hc[0];
       b->stats.rescue_window_skipped = hc[1];
-      HIPCHK(hipStreamSynchronize(s));
       if (nHeavy > b->pairs) throw std::runtime_error("pair choice: heavy-pair count out of range");
       launchPairChoose(nHeavy, samText(b), b->d_oh, b->d_hits, b->d_cig, b->pairs, b->minIns, b->maxIns, b->d_heavy,
                        getenv("GWA_PAIR_SORT_CAP") ? atoi(getenv("GWA_PAIR_SORT_CAP")) : kPairSortCap, b->d_rescue, s);

@@ -62,6 +62,7 @@ __global__ void __launch_bounds__(64) pair_rescue_kernel(IndexView ix, SearchCon
           lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
           lane.qwS = 64;
           lane.initRead(reads.codes + reads.off[r], m);
+          if (m > 256) atomicAdd(heavyCount + 1, 1u);  // rule 3 not tried: mates over 256 bp (gwa.h)
           const int countN = m > 0 && m <= 256 ? lane.buildMasks() : 0x7FFF;
           const int k = lane.k;
           if (m > 0 && m <= 256 && k >= 0 && countN <= k) {  // (QW = 8: mates up to 256 bp are rescued)
@@ -290,13 +291,18 @@ void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream
   hipLaunchKernelGGL(kmer_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ix.occ[fm], ix, K, out);
 }
 
+// the search instances live in search_inst.hip (one translation unit per (QW, R))
+GWA_SEARCH_EXTERN_QW(4)
+GWA_SEARCH_EXTERN_QW(8)
+GWA_SEARCH_EXTERN_QW(16)
+
 void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order,
+                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace, int traceRead) {
   if (reads.n == 0) return;
-  if (QW == 4) launchQuickscanT<4>(ix, cfg, reads, sres, oh, os, searchList, searchCount, order, s, trace, traceRead);
-  else if (QW == 8) launchQuickscanT<8>(ix, cfg, reads, sres, oh, os, searchList, searchCount, order, s, trace, traceRead);
-  else launchQuickscan16(ix, cfg, reads, sres, oh, os, searchList, searchCount, order, s, trace, traceRead);
+  if (QW == 4) launchQuickscanT<4>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
+  else if (QW == 8) launchQuickscanT<8>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
+  else launchQuickscanT<16>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
 }
 
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,
@@ -305,15 +311,16 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
                   const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
                   hipStream_t s, uint32_t *trace, int traceRead) {
   if (n == 0) return;
-  if (QW == 4)
-    launchSearchT<4>(R, ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, work,
-                     ovfList, ovfCount, ovfBits, s, trace, traceRead);
-  else if (QW == 8)
-    launchSearchT<8>(R, ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, work,
-                     ovfList, ovfCount, ovfBits, s, trace, traceRead);
-  else
-    launchSearch16(R, ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, work,
-                   ovfList, ovfCount, ovfBits, s, trace, traceRead);
+#define GWA_L(Q, RR)                                                                                                   \
+  if (QW == Q && R == RR) {                                                                                            \
+    launchSearchQR<Q, RR>(ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, \
+                          work, ovfList, ovfCount, ovfBits, s, trace, traceRead);                                      \
+    return;                                                                                                            \
+  }
+#define GWA_LQ(Q) GWA_L(Q, 4) GWA_L(Q, 8) GWA_L(Q, 16) GWA_L(Q, 32)
+  GWA_LQ(4) GWA_LQ(8) GWA_LQ(16)
+#undef GWA_LQ
+#undef GWA_L
 }
 
 void launchSfSearch(int R, int QW, bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
@@ -322,15 +329,16 @@ void launchSfSearch(int R, int QW, bool wrap, uint32_t lanes, const IndexView &i
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
                     hipStream_t s) {
   if (n == 0) return;
-  if (QW == 4)
-    launchSfSearchT<4>(R, wrap, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
-                       ovfCount, ovfBits, s);
-  else if (QW == 8)
-    launchSfSearchT<8>(R, wrap, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
-                       ovfCount, ovfBits, s);
-  else
-    launchSfSearch16(R, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList,
-                     ovfCount, ovfBits, s);
+#define GWA_L(Q, RR)                                                                                                   \
+  if (QW == Q && R == RR) {                                                                                            \
+    launchSfSearchQR<Q, RR>(wrap, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, \
+                            ovfList, ovfCount, ovfBits, s);                                                            \
+    return;                                                                                                            \
+  }
+#define GWA_LQ(Q) GWA_L(Q, 4) GWA_L(Q, 8) GWA_L(Q, 16) GWA_L(Q, 32)
+  GWA_LQ(4) GWA_LQ(8) GWA_LQ(16)
+#undef GWA_LQ
+#undef GWA_L
 }
 
 size_t laneBytesFor(int R, const Caps &c) {

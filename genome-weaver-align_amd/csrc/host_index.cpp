@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <numeric>
 #include <parallel/algorithm>
 #include <stdexcept>
@@ -217,17 +219,73 @@ struct BV {
 inline int8_t jb(int x) { return (int8_t)(uint8_t)(uint32_t)x; }
 }  // namespace
 
+// words of the table block of one read length (the offsets table, then the raw masks)
+static size_t stairBlockWords(int m, int kmax) {
+  const size_t W = (size_t)(m + 63) / 64;
+  return (size_t)(kmax + 2) * (size_t)(kmax + 1) * ((size_t)(m + kmax + 1) + W);
+}
+
+namespace {
+// Blocks already built, per (read length, kmax): a pipeline creates one batch per chunk of a file
+// and the chunks share their read lengths, so each block is built once per process, not per batch.
+struct StairBlock {
+  std::vector<uint64_t> words;
+  uint64_t threw = 0;
+};
+std::mutex g_stairMu;
+std::map<std::pair<int, int>, std::shared_ptr<const StairBlock>> g_stairCache;
+size_t g_stairCacheWords = 0;
+const size_t kStairCacheWords = (size_t)64 << 20;  // 512 MiB of cached blocks at most
+}  // namespace
+
 void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uint64_t> &tab, std::vector<uint32_t> &base,
                       std::vector<uint64_t> &bad) {
   base.assign(kMaxReadLen + 1, 0xFFFFFFFFu);
   bad.assign(kMaxReadLen + 1, 0);
   tab.clear();
+  {  // every block indexes rows and offsets by the batch's kmax: refuse a table too large to stage
+    size_t words = 0;
+    for (int m : lengths)
+      if (m >= 0 && m <= kMaxReadLen) words += stairBlockWords(m, kmax);
+    if (words > kStairMaxWords)
+      throw std::runtime_error("staircase tables of this batch's read lengths at k " + std::to_string(kmax) + " need " +
+                               std::to_string(words * 8 >> 20) + " MiB (limit " + std::to_string(kStairMaxWords * 8 >> 20) +
+                               " MiB): align reads of very different lengths in separate batches");
+    tab.reserve(words);
+  }
   for (int m : lengths) {
     if (m < 0 || m > kMaxReadLen || base[(size_t)m] != 0xFFFFFFFFu) continue;
+    std::shared_ptr<const StairBlock> blk;
+    {
+      std::lock_guard<std::mutex> g(g_stairMu);
+      auto it = g_stairCache.find({m, kmax});
+      if (it != g_stairCache.end()) blk = it->second;
+    }
+    if (!blk) {
+      auto nb = std::make_shared<StairBlock>();
+      nb->threw = buildStairBlock(m, kmax, nb->words);
+      blk = nb;
+      std::lock_guard<std::mutex> g(g_stairMu);
+      if (g_stairCacheWords + blk->words.size() <= kStairCacheWords) {
+        g_stairCache[{m, kmax}] = blk;
+        g_stairCacheWords += blk->words.size();
+      }
+    }
+    base[(size_t)m] = (uint32_t)tab.size();
+    bad[(size_t)m] = blk->threw;
+    tab.insert(tab.end(), blk->words.begin(), blk->words.end());
+  }
+  if (tab.empty()) tab.push_back(0);
+}
+
+// one read length's block (layout in BsfLane::stairMask / stairMaskRaw); returns bit kk set when
+// StaircaseFilter(m, kk) throws
+uint64_t buildStairBlock(int m, int kmax, std::vector<uint64_t> &tab) {
+  tab.assign(stairBlockWords(m, kmax), 0);
+  {
     const size_t perRow = (size_t)(m + kmax + 1);
-    const size_t start = tab.size();
+    const size_t start = 0;
     const size_t W = (size_t)(m + 63) / 64, rawAt = start + (size_t)(kmax + 2) * (size_t)(kmax + 1) * perRow;
-    tab.resize(rawAt + (size_t)(kmax + 2) * (size_t)(kmax + 1) * W, 0);
     uint64_t threw = 0;  // bit kk: StaircaseFilter(m, kk) throws
     for (int kk = 0; kk <= kmax + 1; ++kk) {
       try {
@@ -260,10 +318,8 @@ void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uin
         threw |= 1ULL << kk;
       }
     }
-    base[(size_t)m] = (uint32_t)start;
-    bad[(size_t)m] = threw;
+    return threw;
   }
-  if (tab.empty()) tab.push_back(0);
 }
 
 }  // namespace gwa

@@ -36,8 +36,13 @@ void finishIndex(HostIndex &ix);
 // StaircaseFilter(m, kk) constructor throws in the reference (bit kk of bad[m]; its table is zeros).
 // Behind each length's table: the staircase masks themselves, ceil(m / 64) words per (kk, row)
 // (offsets outside [-kmax, m], which only chunks with wrapped (byte) starts reach)
+// Blocks are cached per (m, kmax) across batches; a batch whose tables exceed kStairMaxWords fails
+// with an error naming the size (reads of many lengths at a large k: split the batch by length).
 void buildStairTables(const std::vector<int> &lengths, int kmax, std::vector<uint64_t> &tab, std::vector<uint32_t> &base,
                       std::vector<uint64_t> &bad);
+// one length's block (offsets table, then raw masks) into tab; bit kk set: StaircaseFilter(m, kk) throws
+uint64_t buildStairBlock(int m, int kmax, std::vector<uint64_t> &tab);
+static const size_t kStairMaxWords = (size_t)128 << 20;  // 1 GiB of tables per batch at most
 
 // Java-String.compareTo-consistent ranks of contig names
 void rankNames(HostIndex &ix);

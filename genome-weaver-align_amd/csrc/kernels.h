@@ -11,7 +11,7 @@ namespace gwa {
 struct Caps;
 
 void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order,
+                     const OutSlots &os, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace = nullptr, int traceRead = -1);
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,

@@ -1,6 +1,6 @@
-// search_kernels.h -- the per-read search kernels of the align path (gwa_kernels.hip), as templates
-// instantiated by gwa_kernels.hip (query words QW = 4, 8: reads <= 256 bp) and gwa_kernels_long.hip
-// (QW = 16: reads <= 512 bp), so the long-read instances compile in their own translation unit.
+// search_kernels.h -- the per-read search kernels of the align path, as templates instantiated by
+// search_inst.hip once per (query words QW = 4, 8, 16: reads <= 128, 256, 512 bp; NFA rows R), each
+// pair in its own translation unit; gwa_kernels.hip dispatches to them.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -29,13 +29,11 @@ template <int QW>
 __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
                                                            OutHeader *oh, OutSlots os,
                                                            uint32_t *searchList, uint32_t *searchCount,
-                                                           const uint32_t *order, uint32_t *trace, int traceRead) {
-  // lane i scans read order[i] (reads sorted by their first k-mer: neighbouring lanes start on
-  // neighbouring suffix-array rows, gwa_batch_run) or read i
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t r = (order && i < reads.n) ? order[i] : i;
+                                                           uint32_t *trace, int traceRead) {
+  // lane r scans read r
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   bool need = false;
-  if (i < reads.n) {
+  if (r < reads.n) {
     const uint32_t o = reads.off[r];
     const int m = (int)reads.len[r];
     OutHeader *h = oh + r;
@@ -103,36 +101,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
     for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
     __syncthreads();
   }
-#ifdef GWA_PERREAD_KERNEL
-  {
-    const uint32_t rounds = (n + total - 1) / total;
-    for (uint32_t it = 0; it < rounds; ++it) {
-      const uint32_t i = gid + it * total;
-      bool ovf = false;
-      uint32_t r = 0;
-      if (i < n) {
-        r = list[i];
-        const uint32_t o = reads.off[r];
-        const int m = (int)reads.len[r];
-        BsfLane<R, QW, (LH != 0 && R >= 8)> lane(ix, cfg, st, L, caps);
-        lane.chrRank = chrRank;
-        if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
-        __shared__ uint64_t qwLds1[2 * QW * 256];
-        lane.qwL = (lds_u64 *)(qwLds1 + threadIdx.x);
-        lane.qwS = 256;
-        if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
-        lane.initRead(reads.codes + o, m);
-        lane.searchPhase(sres[r]);
-        lane.writeSearchOutput(oh + r, os, r);
-        if (lane.trace) trace[0] = (uint32_t)lane.traceN;
-        ovf = oh[r].status == ST_OVERFLOW;
-        if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
-      }
-      waveAppend(ovf, r, ovfList, ovfCount);
-    }
-    return;
-  }
-#endif
   typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8))> Lane;  // hybrid heap: k >= 4 with the LDS heap, sparse tiers
   Lane lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
@@ -286,75 +254,64 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
 
 template <int QW>
 void launchQuickscanT(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order, hipStream_t s,
-                      uint32_t *trace, int traceRead) {
+                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
+                      int traceRead) {
   hipLaunchKernelGGL(fm_quickscan_kernel<QW>, dim3((reads.n + 255) / 256), dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
-                     searchList, searchCount, order, trace, traceRead);
+                     searchList, searchCount, trace, traceRead);
 }
 
-template <int QW>
-void launchSearchT(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
-                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
-                   uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank,
-                   uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s,
-                   uint32_t *trace, int traceRead) {
+// one (QW, R) instance set per translation unit (search_inst.hip, built once per pair by the
+// Makefile): the bsf_search kernels of the three heap kinds and the sf_search kernels
+template <int QW, int R>
+void launchSearchQR(int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+                    const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
+                    uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank,
+                    uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s,
+                    uint32_t *trace, int traceRead) {
   dim3 grid((lanes + 255) / 256);
-  const int key = R * 3 + (ldsHeap == 2 ? 2 : ldsHeap ? 1 : 0);
-  switch (key) {
-#define GWA_CASE(RR, LL)                                                                                               \
-  case RR * 3 + LL:                                                                                                    \
-    hipLaunchKernelGGL((bsf_search_kernel<RR, QW, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,      \
-                       scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, trace, traceRead); \
-    break;
-#define GWA_CASE2(RR) GWA_CASE(RR, 0) GWA_CASE(RR, 1) GWA_CASE(RR, 2)
-    GWA_CASE2(4)
-    GWA_CASE2(8)
-    GWA_CASE2(16)
-    GWA_CASE2(32)
-#undef GWA_CASE2
+#define GWA_CASE(LL)                                                                                                   \
+  hipLaunchKernelGGL((bsf_search_kernel<R, QW, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n, scratch,  \
+                     laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, trace, traceRead)
+  if (ldsHeap == 2) GWA_CASE(2);
+  else if (ldsHeap) GWA_CASE(1);
+  else GWA_CASE(0);
 #undef GWA_CASE
-    default: break;
-  }
 }
 
 // wrap: the batch has reads whose prefix-scan chunks wrap (sfChunksWrap: some lengths of 129-256 bp,
 // and reads of <= 31 bp at a large k); QW = 16 reads are always run with the WRAP path
-template <int QW>
-void launchSfSearchT(int R, bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
-                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
-                     const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
-                     uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s) {
-  dim3 grid((lanes + 255) / 256);
-  constexpr bool kAlways = QW == 16;
-  const int key = R * 2 + ((kAlways || wrap) ? 1 : 0);
-  switch (key) {
-#define GWA_SF(RR, WW)                                                                                                 \
-  case RR * 2 + WW:                                                                                                    \
-    if (WW || !kAlways)                                                                                                \
-      hipLaunchKernelGGL((sf_search_kernel<RR, QW, WW ? true : kAlways>), grid, dim3(256), 0, s, ix, cfg, st, reads,   \
-                         list, n, scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);      \
-    break;
-    GWA_SF(4, 0) GWA_SF(4, 1)
-    GWA_SF(8, 0) GWA_SF(8, 1)
-    GWA_SF(16, 0) GWA_SF(16, 1)
-    GWA_SF(32, 0) GWA_SF(32, 1)
-#undef GWA_SF
-    default: break;
-  }
-}
-
-// the QW = 16 instances (gwa_kernels_long.hip)
-void launchQuickscan16(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
-                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, const uint32_t *order,
-                       hipStream_t s, uint32_t *trace, int traceRead);
-void launchSearch16(int R, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
-                    const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
-                    uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank,
-                    uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s,
-                    uint32_t *trace, int traceRead);
-void launchSfSearch16(int R, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
+template <int QW, int R>
+void launchSfSearchQR(bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                       const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                       const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
-                      uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s);
+                      uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s) {
+  dim3 grid((lanes + 255) / 256);
+  if (wrap || QW == 16)
+    hipLaunchKernelGGL((sf_search_kernel<R, QW, true>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,
+                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);
+  else if (QW != 16)
+    hipLaunchKernelGGL((sf_search_kernel<R, QW, QW == 16>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,
+                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);
+}
+
+// explicit instantiation (search_inst.hip: `template`) or declaration (`extern template`) of one
+// (QW, R) instance set
+#define GWA_SEARCH_INSTANCE(KW, QW_, R_)                                                                           \
+  KW void launchSearchQR<QW_, R_>(int, uint32_t, const IndexView &, const SearchConfig &, const StairTables &,     \
+                                  const ReadsView &, const ScanRes *, const uint32_t *, uint32_t, uint8_t *, uint64_t, \
+                                  const Caps &, OutHeader *, const OutSlots &, const int32_t *, uint32_t *,        \
+                                  uint32_t *, uint32_t *, uint32_t *, hipStream_t, uint32_t *, int);               \
+  KW void launchSfSearchQR<QW_, R_>(bool, uint32_t, const IndexView &, const SearchConfig &, const StairTables &,  \
+                                    const ReadsView &, const uint32_t *, uint32_t, uint8_t *, uint64_t,           \
+                                    const Caps &, OutHeader *, const OutSlots &, const int32_t *, uint32_t *,      \
+                                    uint32_t *, uint32_t *, uint32_t *, hipStream_t);
+#define GWA_SEARCH_EXTERN_QW(QW_)                                                                                  \
+  GWA_SEARCH_INSTANCE(extern template, QW_, 4)                                                                    \
+  GWA_SEARCH_INSTANCE(extern template, QW_, 8)                                                                    \
+  GWA_SEARCH_INSTANCE(extern template, QW_, 16)                                                                   \
+  GWA_SEARCH_INSTANCE(extern template, QW_, 32)                                                                   \
+  extern template void launchQuickscanT<QW_>(const IndexView &, const SearchConfig &, const ReadsView &, ScanRes *, \
+                                             OutHeader *, const OutSlots &, uint32_t *, uint32_t *, hipStream_t,   \
+                                             uint32_t *, int);
 
 }  // namespace gwa

@@ -118,8 +118,9 @@ typedef struct {
   double format_ms;        /* the last SAM formatting of the batch on the device (gwa_batch_format / results) */
   double rescue_ms;        /* paired-end batches: pair choice + mate rescue kernels (part of kernel_ms) */
   uint64_t heavy_pairs;    /* paired-end batches: pairs chosen by the sorted sweep (> 64 candidate combinations) */
-  uint64_t rescue_window_skipped; /* paired-end: mate rescues not tried because the window the insert range
-                                   * allows (max_insert - min_insert + m + 2 kr) exceeds 320 bases */
+  uint64_t rescue_window_skipped; /* paired-end: mate rescues not tried, because the mate is longer than
+                                   * 256 bp or the window the insert range allows (max_insert - min_insert
+                                   * + m + 2 kr) exceeds 320 bases */
 } gwa_batch_stats_t;
 
 void gwa_config_default(gwa_config_t *cfg);
@@ -171,8 +172,8 @@ int gwa_batch_run(gwa_batch_t *b);
  * pairs, line_off per pair) with mate fields and TLEN.
  * Mate rescue (rule 3) aligns the other mate inside the window the insert range allows next to the
  * anchor; it is tried for mates of at most 256 bp and windows of at most 320 bases (max_insert -
- * min_insert + m + 2 max(k, m / 10); the default 210-390 gives 300 for 100 bp mates).  Wider windows
- * skip the rescue and are counted in gwa_batch_stats_t.rescue_window_skipped. */
+ * min_insert + m + 2 max(k, m / 10); the default 210-390 gives 300 for 100 bp mates).  Longer mates
+ * and wider windows skip the rescue and are counted in gwa_batch_stats_t.rescue_window_skipped. */
 int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t *mate1, const gwa_reads_t *mate2,
                            int32_t min_insert, int32_t max_insert, gwa_batch_t **out);
 /* One call per paired batch: create_pairs + run + results. */
