@@ -63,10 +63,17 @@ inline FILE *gwaVerifyLog() {
     if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) prof[w] += 1;       \
     prof[l] += 1;                                                               \
   } while (0)
+// GWA_PW(w, e, b): a store of b bytes at one site: bytes in slot w, one lane event in slot e
+#define GWA_PW(w, e, b)                                                         \
+  do {                                                                          \
+    prof[w] += (uint64_t)(b);                                                   \
+    prof[e] += 1;                                                               \
+  } while (0)
 #else
 #define GWA_PT(v)
 #define GWA_PA(r, v)
 #define GWA_PC(w, l)
+#define GWA_PW(w, e, b)
 #endif
 
 // LDS-typed pointers on the device (plain pointers on host builds)
@@ -796,6 +803,7 @@ struct BsfLane {
   GWA_HD int minK(int s) { return (int)(((uint32_t)S(s).state >> 8) & 0xFF); }
   GWA_HD void setMinK(int s, int d) {
     invalidateCache();
+    GWA_PW(PR_WS, PR_ES, 4);
     S(s).state &= ~(0xFF << 8);
     S(s).state |= (d & 0xFF) << 8;
   }
@@ -822,6 +830,7 @@ struct BsfLane {
   static constexpr int32_t kStRef = 1 << 26;
   GWA_HD void markRef(int s) {
     if (s == cacheIdx) flushCache();  // a referenced state is never a deferred one
+    GWA_PW(PR_WS, PR_ES, 4);
     S(s).state |= kStRef;
     if (s == cacheIdx) cache.state |= kStRef;
   }
@@ -832,6 +841,7 @@ struct BsfLane {
   GWA_HD int newInitial(int strand, int dir, int start, int end, int cur, int piv, int priority) {
     int id = allocState();
     if (id < 0) return -1;
+    GWA_PW(PR_WA, PR_EA, sizeof(DState<R>));
     DState<R> &d = S(id);
     d.meta = 0;
     setCursor(d, strand, dir, start, end, cur, piv);
@@ -1210,6 +1220,7 @@ struct BsfLane {
   // ---- hits (R/ReadHit.java) ----
   GWA_HD int newHit(int32_t chr, int32_t pos, int ml, int qs, int qe, int diff, int strand, int cigOff, int cigLen, int numHits) {
     if (nHits >= caps.hits) { ovf(OV_HITS); return -1; }
+    GWA_PW(PR_WH, PR_EH, sizeof(DHit));
     DHit &h = L.hits()[nHits];
     h.chr = chr; h.pos = pos; h.matchLength = ml; h.qStart = qs; h.qEnd = qe; h.diff = diff; h.strand = strand;
     h.numHits = numHits; h.next = -1; h.cigarOff = cigOff; h.cigarLen = cigLen; h.pad = 0;
@@ -1217,6 +1228,7 @@ struct BsfLane {
   }
   GWA_HD int putCigarOp(int type, int len) {
     if (nCigar >= caps.cigar) { ovf(OV_CIGAR); return -1; }
+    GWA_PW(PR_WH, PR_EH, 2);
     L.cigar()[nCigar++] = (uint16_t)((len << 3) | type);
     return 0;
   }
@@ -1259,10 +1271,11 @@ struct BsfLane {
     int n = keep;
     for (int i = keep; i < listSize; ++i) {
       int e = L.list()[i];
-      if (hitTotalDiff(e) <= minMismatches && hitTotalMatch(e) >= maxMatchLength) L.list()[n++] = e;
+      if (hitTotalDiff(e) <= minMismatches && hitTotalMatch(e) >= maxMatchLength) { GWA_PW(PR_WH, PR_EH, 4); L.list()[n++] = e; }
     }
     listOk = n;
     if (n >= caps.list) { ovf(OV_LIST); listSize = n; return; }
+    GWA_PW(PR_WH, PR_EH, 4);
     L.list()[n++] = hit;
     listSize = n;
   }
@@ -1289,6 +1302,7 @@ struct BsfLane {
       }
       arr[j + 1] = x;
     }
+    GWA_PW(PR_WH, PR_EH, 4 * n);
     for (int i = 0; i + 1 < n; ++i) L.hits()[arr[i]].next = arr[i + 1];
     L.hits()[arr[n - 1]].next = -1;
     return arr[0];
@@ -1316,17 +1330,9 @@ struct BsfLane {
 
   // ---- BitParallelSmithWaterman.alignBlockDetailed (A/BitParallelSmithWaterman.java:141-147,335-644) ----
   // query = q[strand][qs,qe) (reversed for strand 1), ref = T[refStart, refEnd)
-  // refCode through a one-word cache of the 2-bit text and of the N bitmap (the run-ahead's text
-  // walk moves one position per step: one load per 32 / 64 steps)
-  int tcOn = 0;
+  // a one-word cache of the 2-bit text and of the N bitmap for the text-mode FM steps (nextSi)
   int64_t tcW2 = -1, tcWN = -1;
   uint64_t tcC2 = 0, tcCN = 0;
-  GWA_HD int refCodeCached(int64_t p) {
-    const int64_t a = p >> 5, b = p >> 6;
-    if (a != tcW2) { tcC2 = ix.text2[a]; tcW2 = a; }
-    if (b != tcWN) { tcCN = ix.textN[b]; tcWN = b; }
-    return ((tcCN >> (p & 63)) & 1) ? 4 : (int)((tcC2 >> ((p & 31) * 2)) & 3);
-  }
   GWA_HD int refCode(int64_t p) const {
     uint64_t nb = ix.textN[p >> 6];
     if ((nb >> (p & 63)) & 1) return 4;
@@ -1487,12 +1493,17 @@ struct BsfLane {
           const int s0 = r0 < 0 ? 0 : r0 > 32 ? 32 : r0, s1 = r1 < 0 ? 0 : r1 > 32 ? 32 : r1;
           const uint64_t msk = ((s1 >= 32 ? 0xFFFFFFFFULL : (1ULL << s1) - 1ULL) & ~((1ULL << s0) - 1ULL));
           *hc8 = (lastWord | msk) & ~(msk << 32);
+          GWA_PW(PR_WD, PR_ED, 8);
         }
         const int lo1 = j - c0 - 16;
         lastWord = (uint64_t)rows32(vp, lo1) | ((uint64_t)rows32(vn, lo1) << 32);
         hc8[is] = lastWord;
+        GWA_PW(PR_WD, PR_ED, 8);
+        GWA_PC(PR_EDW, PR_N - 2);
       } else {
-        if (act) hc[(size_t)actBlock * is] = VpVn{~0ULL, 0ULL};
+        if (act) { GWA_PW(PR_WD, PR_ED, 16); hc[(size_t)actBlock * is] = VpVn{~0ULL, 0ULL}; }
+        GWA_PW(PR_WD, PR_ED, 16 * bMax);
+        GWA_PC(PR_EDW, PR_N - 2);
 #pragma unroll
         for (int r = 0; r < DB; ++r)
           if (r < bMax) hc[colStep + r * is] = VpVn{vp[r], vn[r]};
@@ -1535,7 +1546,7 @@ struct BsfLane {
           curL += cnt;
         } else {
           if (nCigar + 2 * nRuns + 4 > cap) bad = 1;
-          else cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
+          else { GWA_PW(PR_WH, PR_EH, 2); cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT); }
           ++nRuns;
           curT = t;
           curL = cnt;
@@ -1609,6 +1620,7 @@ struct BsfLane {
     } else {
       if (nCigar + 2 * nRuns + 4 > cap) { ovf(OV_CIGAR); return -1; }
       cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
+      GWA_PW(PR_WH, PR_EH, 2 * (lastM + 2));
       diff -= adj + pendAdj;
       if (pendL > 0 && putCigarOp(4, pendL) < 0) return -1;
       for (int i = lastM; i >= 0; --i) cg[nCigar++] = cg[cap - 1 - i];
@@ -1705,6 +1717,7 @@ struct BsfLane {
     int h = newHit(chr, p, frag, d.start, d.end, diff, strand, co, cl, (int)(d.curUb - d.curLb));
     if (h < 0) return -2;
     if (memo) {
+      GWA_PW(PR_WH, PR_EH, 12);
       L.hits()[h].pad = (int32_t)mkey;
       L.cand()[mslot] = (int64_t)(h + 1);
     }
@@ -1720,6 +1733,7 @@ struct BsfLane {
       if (res == -2) return false;
       if (first) { al = res; continue; }
       if (al < 0) { status = ST_ERROR; return false; }
+      GWA_PW(PR_WH, PR_EH, 4);
       L.hits()[al].next = res;  // nextHit is never advanced (:567-571)
     }
     if (al < 0) { status = ST_ERROR; return false; }
@@ -1864,12 +1878,13 @@ struct BsfLane {
     uint64_t rl = hasF ? fl : bl, ru = hasF ? fu : bu;
     rl = rl > ix.N ? ix.N : rl;
     ru = ru > ix.N ? ix.N : ru;
-    uint64_t w2 = 0, wN = 0;
     Block B0, B1;
-    const int tc = tcOn | cfg.textCache;  // text words through the lane's one-word cache (refCodeCached)
-    if (kind == K_TEXT && !tc) {
-      w2 = ix.text2[p >> 5];
-      wN = ix.textN[p >> 6];
+    // text words through the lane's one-word cache (a text-mode run moves one position per step: one
+    // load per 32 / 64 steps), the loads issued here, before `between`
+    if (kind == K_TEXT) {
+      const int64_t a = p >> 5, b = p >> 6;
+      if (a != tcW2) { tcC2 = ix.text2[a]; tcW2 = a; }
+      if (b != tcWN) { tcCN = ix.textN[b]; tcWN = b; }
     }
     if (kind == K_RANK) {
       loadBlock(ix.occ[fmR], rl >> 7, B0);
@@ -1882,7 +1897,7 @@ struct BsfLane {
       d.meta |= M_TEXT | (hasF ? (hasB ? SI_BID : SI_FWD) : SI_BWD);
       d.lb[0] = (uint32_t)t;
       d.lb[1] = (uint32_t)len;
-      d.lb[2] = (uint32_t)(tc ? refCodeCached(p) : ((wN >> (p & 63)) & 1) ? 4 : (int)((w2 >> ((p & 31) * 2)) & 3));
+      d.lb[2] = (uint32_t)(((tcCN >> (p & 63)) & 1) ? 4 : (int)((tcC2 >> ((p & 31) * 2)) & 3));
       d.lb[3] = 0;
       for (int i = 0; i < 4; ++i) d.ub[i] = 0;
       d.bBase = 0;
@@ -1966,6 +1981,7 @@ struct BsfLane {
       t.state |= 1 << 25;  // updateClippedFlag
     }
     t.state |= kStRef;  // a's nextSplit
+    GWA_PW(PR_WA, PR_EA, 2 * sizeof(DState<R>));
     S(a) = d;
     S(b) = t;
     // keyOf(a) for the chain [a -> b] from the registers (chainScore with one split)
@@ -1984,6 +2000,7 @@ struct BsfLane {
       prev = S(prev).nextSplit;
       if (prev < 0) return -1;
     }
+    GWA_PW(PR_WS, PR_ES, 4);
     S(prev).nextSplit = newS;
     if (newS >= 0) markRef(newS);
     refreshKeysFor(prev);  // score() of every chain through prev changed
@@ -2085,21 +2102,44 @@ struct BsfLane {
     upperSearches = m * 20;
     return true;
   }
-  // One call = one micro-step of the loop of align_internal (:343-477).  A poll is followed by at
-  // most ONE child expansion (an FM step); the remaining children of the same poll and the split /
-  // clip children come in later calls (xMode 1 / 2), so every lane of a wavefront performs about
-  // one FM step per call instead of the wavefront looping until its slowest lane has tried all
-  // four bases.  Nothing else touches a lane between its micro-steps, so the order of operations
-  // on its heap and arena is exactly the reference's.
+  // One call = one micro-step of the loop of align_internal (:343-477) with at most ONE FM step, and
+  // that step at ONE call site (buildChild below): every lane of a wavefront that has an FM step to
+  // take in this call takes it there together, whichever part of the loop it came from -- the child
+  // of a poll (xMode 1), or the next step of a run-ahead (xMode 3).  The control work before it
+  // (poll, pruning, the choice of the child, the split / clip children) runs per lane for up to
+  // two rounds (controlPass), so a lane whose poll ends in a prune or a split still reaches the FM step
+  // of this call.  Nothing else touches a lane between its micro-steps, so the order of operations on its
+  // heap and arena is exactly the reference's.
   // (the expanded state xC is re-read from the arena / cache at each micro-step rather than kept
   // in the lane object: its flag word is always stored, so the arena copy is current)
-  int xMode = 0, xT = 0, xBase = 0, xC = 0, xNm = 0, xNextBase = 0;
-  GWA_HD int searchStep() {
+  int xMode = 0, xT = 0, xBase = 0, xC = 0, xNm = 0, xNextBase = 0, xFirst = 0;
+  // run-ahead (xMode 3): the queue's bound (heapNoop), steps taken, whether the cached state moved,
+  // the run's first state
+  uint64_t raBound = 0;
+  int raIt = 0, raMoved = 0, raNs = -1;
+  // one round of the control work of a micro-step (searchStep): CP_STEP when it ends at an FM step
+  // (its parent in P, its base in ch), CP_AGAIN when it ended without one (a prune, the split / clip
+  // children, the end of a run-ahead), else CP_DONE / CP_REPORT
+  enum { CP_AGAIN = 0, CP_STEP = 1, CP_DONE = 2, CP_REPORT = 3 };
+  GWA_HD int controlPass(DState<R> &P, int &ch, int &kind) {
+    if (xMode == 3) {
+      const int nb = raNext();
+      if (nb >= 0) {  // the next step of the run (the checks of :352-396 passed for the cached state)
+        P = cache;
+        ch = nb;
+        kind = 2;
+        return CP_STEP;
+      }
+      const int ns = raFinish();
+      if (ns == -2) return CP_DONE;
+      queueAdd(update(xBase, xC, ns));
+      xMode = 0;
+      return CP_AGAIN;
+    }
     DState<R> xCS;
     if (xMode == 0) {
-      GWA_PC(PR_NSW, PR_NSL);
-      if (!(heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR)) return SS_DONE;
-      if (numFMIndexSearches > upperSearches) return SS_DONE;
+      if (!(heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR)) return CP_DONE;
+      if (numFMIndexSearches > upperSearches) return CP_DONE;
       GWA_PT(tp);
       const int base = queuePoll();
       if (base != cacheIdx) flushCache();  // the deferred state stays queued
@@ -2120,14 +2160,14 @@ struct BsfLane {
       if ((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) {
         flushCache();  // verify reads the chain from the arena
         pendingBase = base;
-        return SS_REPORT;
+        return CP_REPORT;
       }
       // the checks below drop the polled state (a deferred one is chain-free: dead from here)
       const int nm = (int)(((uint32_t)C.state >> 8) & 0xFF);
       if ((C.state & 0x1F) == 0x1F || nm > minMismatches || minMismatches - nm < 0 || ubScore < 0 ||
           ubScore < bestScore) {  // isFinished / pruned
         dropIfCached(base);
-        return SS_CONTINUE;
+        return CP_AGAIN;
       }
       xBase = base;
       xC = c;
@@ -2142,47 +2182,28 @@ struct BsfLane {
     if (xMode == 1) {
       // children (:386-410): nextBase first -- a state from it ends the iteration -- then every
       // base still unchecked; one FM step per call
-      GWA_PT(te);
       // (the checked flags are stored once, with the child taken below or with the split flag: nothing
       // reads the arena copy of xC in between, siIsEmpty reads the register copy)
-      int ch = -1, tt = xT, zero = 0;
-      for (; tt < 4 && ch < 0; ++tt) {
+      int c2 = -1, tt = xT, zero = 0;
+      for (; tt < 4 && c2 < 0; ++tt) {
         zero |= tt == 0 ? 1 : 0;  // (single-exit loop, integer state: see quickScan)
         const int cand = tt < 0 ? xNextBase : tt;
         if (xCS.state & (1 << cand)) continue;  // isChecked
         xCS.state |= 1 << cand;                 // updateFlag
         if (siIsEmpty(xCS, cand)) continue;
-        ch = cand;
+        c2 = cand;
       }
       // StaircaseFilter sf = getStairCaseFilter(m) where the loop over every base begins (:439); this
       // micro-step entered it if it ran the loop at tt = 0
-      if (zero && !stairOk()) return SS_DONE;
-      const int first = (xT < 0 && tt == 0) ? 1 : 0;  // the child taken is nextBase
+      if (zero && !stairOk()) return CP_DONE;
+      xFirst = (xT < 0 && tt == 0) ? 1 : 0;  // the child taken is nextBase
       xT = tt;
-      if (ch >= 0) {
+      if (c2 >= 0) {
         storeStateWord(xC, xCS.state);
-        GWA_PT(tn);
-        int ns = nextStateLocal(xC, xCS, ch, first && xC == xBase && deferrable(xCS));
-        GWA_PA(PR_LOOP, tn);
-        if (ns == -2) return SS_DONE;
-        if (ns >= 0) {
-          if (first && xC == xBase) {
-            GWA_PT(tra);
-            ns = runAhead(ns);
-            GWA_PA(PR_BOUND, tra);
-            if (ns == -2) return SS_DONE;
-          }
-          GWA_PT(tad);
-          queueAdd(update(xBase, xC, ns));
-          GWA_PA(PR_ADD1, tad);
-          if (first) {
-            xMode = 0;
-            GWA_PA(PR_EXP1, te);
-            return SS_CONTINUE;
-          }
-        }
-        GWA_PA(PR_EXPN, te);
-        if (xT < 4) return SS_CONTINUE;  // more candidates: next call
+        P = xCS;
+        ch = c2;
+        kind = 1;
+        return CP_STEP;
       }
       xMode = 2;
     }
@@ -2198,7 +2219,7 @@ struct BsfLane {
         for (int clip = 0; clip < 2; ++clip) {  // split, then clip (:414-425)
           uint64_t key = 0;
           const int ns = nextStateAfterSplit(xCS, clip != 0, &key);
-          if (ns == -2) return SS_DONE;
+          if (ns == -2) return CP_DONE;
           if (ns >= 0) {
             if (xC == xBase) queueAddKeyed((key << KS) | (uint64_t)ns);  // update(base, base, ns) == ns
             else queueAdd(update(xBase, xC, ns));
@@ -2208,6 +2229,68 @@ struct BsfLane {
     }
     if (xC == xBase && deferrable(xCS)) dropIfCached(xC);  // the expanded chain-free state is done
     GWA_PA(PR_SPLIT, ts);
+    return CP_AGAIN;
+  }
+  GWA_HD int searchStep() {
+    DState<R> P;  // the parent of this call's FM step (a register copy)
+    int ch = -1, kind = 0;  // the FM step's base; kind 1: a child of xC, 2: a run-ahead step
+    GWA_PC(PR_NSW, PR_NSL);
+    // kPasses = 2 rounds of control work, written out (no loop: early exits from divergent loops
+    // have been mis-lowered on gfx950)
+    int cp = controlPass(P, ch, kind);
+    if (cp == CP_AGAIN) cp = controlPass(P, ch, kind);
+    if (cp == CP_DONE) return SS_DONE;
+    if (cp == CP_REPORT) return SS_REPORT;
+    if (cp != CP_STEP) return SS_CONTINUE;
+    const int fm0 = numFMIndexSearches, ts0 = textSteps;
+    // ---- the FM step of this call: next(c, ch) and the automaton step, SearchState.nextState ----
+    GWA_PT(tn);
+    DState<R> d;
+    const bool ok = buildChild(P, ch, d);
+    GWA_PA(PR_LOOP, tn);
+    if (kind == 2) {  // run-ahead
+      if (!ok) {  // a rejected first child: the state goes through the loop as the reference runs it
+        numFMIndexSearches = fm0;
+        textSteps = ts0;
+        raIt = cfg.runAheadMax;  // the run ends at the next call
+      } else {
+        cache = d;
+        raMoved = 1;
+        ++raIt;
+      }
+      return SS_CONTINUE;
+    }
+    // a child of xC (nextStateLocal): in a new arena slot, cached.  When xC is the polled chain-free
+    // state and this child is its accepted next base, the reference drops xC: a deferred xC is not
+    // written back
+    int ns = -1;
+    if (ok) {
+      const int id = allocState();
+      if (id < 0) return SS_DONE;
+#ifndef GWA_NO_CACHE
+      if (xFirst && xC == xBase && deferrable(P) && xC == cacheIdx) cacheDirty = 0;
+      flushCache();
+      cache = d;
+      cacheIdx = id;
+      if (deferrable(d)) cacheDirty = 1;
+      else { GWA_PW(PR_WA, PR_EA, sizeof(DState<R>)); L.arena()[id] = d; }
+#else
+      L.arena()[id] = d;
+#endif
+      ns = id;
+    }
+    if (ns >= 0) {
+      if (xFirst && xC == xBase && raStart(ns)) {  // its next steps run ahead (xMode 3)
+        xMode = 3;
+        return SS_CONTINUE;
+      }
+      queueAdd(update(xBase, xC, ns));
+      if (xFirst) {
+        xMode = 0;
+        return SS_CONTINUE;
+      }
+    }
+    if (xT >= 4) xMode = 2;  // no candidate left: the split / clip children next
     return SS_CONTINUE;
   }
 
@@ -2222,6 +2305,7 @@ struct BsfLane {
   DState<R> cache;
   GWA_HD void flushCache() {
     if (cacheDirty) {
+      GWA_PW(PR_WA, PR_EA, sizeof(DState<R>));
       L.arena()[cacheIdx] = cache;
       cacheDirty = 0;
     }
@@ -2236,7 +2320,7 @@ struct BsfLane {
 #endif
   }
   GWA_HD void storeStateWord(int idx, int32_t w) {
-    if (!(idx == cacheIdx && cacheDirty)) L.arena()[idx].state = w;
+    if (!(idx == cacheIdx && cacheDirty)) { GWA_PW(PR_WS, PR_ES, 4); L.arena()[idx].state = w; }
     if (idx == cacheIdx) cache.state = w;
   }
   GWA_HD void invalidateCache() {
@@ -2267,6 +2351,7 @@ struct BsfLane {
     // independent (both read only the parent), so the automaton step runs while the FM step's
     // reads are in flight.  Counts and results are those of the reference order.
     bool nfaOk = false;
+    GWA_PC(PR_NBW, PR_NBL);
     GWA_PT(tf);
     nextSi(cs, ch, d, [&] {
       GWA_PT(tq);
@@ -2300,27 +2385,6 @@ struct BsfLane {
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
     return true;
   }
-  // the child in a new arena slot (stays cached); -1 null, -2 overflow.  parentDead: c is the
-  // polled chain-free state and this child is its accepted next base (the reference drops c), so a
-  // deferred c is not written back
-  GWA_HD int nextStateLocal(int c, const DState<R> &cs, int ch, bool parentDead) {
-    DState<R> d;
-    if (!buildChild(cs, ch, d)) return -1;
-    int id = allocState();
-    if (id < 0) return -2;
-#ifndef GWA_NO_CACHE
-    if (parentDead && c == cacheIdx) cacheDirty = 0;
-    flushCache();
-    cache = d;
-    cacheIdx = id;
-    if (deferrable(d)) cacheDirty = 1;
-    else L.arena()[id] = d;
-#else
-    L.arena()[id] = d;
-#endif
-    return id;
-  }
-
   // ---- run-ahead over text-mode match runs ----
   // When the polled state's first child (its own next base, :386-396) is accepted, the reference
   // pushes it and ends the iteration; the next poll usually returns that child, whose first child
@@ -2363,53 +2427,44 @@ struct BsfLane {
   GWA_HD uint64_t keyOfLocal(const DState<R> &c) const {  // keyOf of a chain-free state
     return packKey((int)(((uint32_t)c.state >> 16) & 0xFF), stateScore(c, 0, false), cProcessed(c));
   }
-  GWA_HD int runAhead(int ns) {
-#ifdef GWA_NO_RA
-    return ns;
-#endif
-    if (cfg.runAheadMax <= 0 || cacheIdx != ns || cache.nextSplit >= 0 || !siText(cache)) return ns;
-    uint64_t bound;
-    if (!heapNoop(&bound)) return ns;
-    // the run works on the register copy `cache` (the state to be polled next) in place
-    int moved = 0;
-    if (!cfg.textCache) tcW2 = tcWN = -1;
-    for (int it = 0; it < cfg.runAheadMax; ++it) {
-      // loop top (:352-356) and the poll checks (:358-385) for the cached state
-      if (numFMIndexSearches > upperSearches || status == ST_OVERFLOW || status == ST_ERROR) break;
-      if (keyOfLocal(cache) >= bound) break;
-      if ((((uint32_t)cache.state >> 24) & 3) != 0 || cRemaining(cache) == 0) break;
-      if ((cache.state & 0x1F) == 0x1F) break;
-      const int nm = (int)(((uint32_t)cache.state >> 8) & 0xFF);
-      if (nm > minMismatches) break;
-      const int ubs = stateScore(cache, 0, true);
-      if (ubs < 0 || ubs < bestScore) break;
-      if (!siText(cache)) break;
-      const int nb = qcode(cStrand(cache), cNextIdx(cache));
-      if ((cache.state & (1 << nb)) != 0 || siIsEmpty(cache, nb)) break;
-      // (the parent's checked flag for nb is not recorded: the parent is never read again, and the
-      // child takes only the priority bits of the parent's state word)
-      DState<R> d;
-      const int fm0 = numFMIndexSearches, ts0 = textSteps;
-      tcOn = 1;
-      const bool ok = buildChild(cache, nb, d);
-      tcOn = 0;
-      if (!ok) {  // a rejected first child: the state goes through the loop as the reference runs it
-        numFMIndexSearches = fm0;
-        textSteps = ts0;
-        break;
-      }
-      cache = d;
-      moved = 1;
-    }
-    if (!moved) return ns;
-    // ns (the run's first state, deferred or written) is never referenced: the run's last state
-    // takes its place in the queue
+  // a run starts from the child ns just created (cached) when the queue provably comes back unchanged
+  GWA_HD bool raStart(int ns) {
+    if (cfg.runAheadMax <= 0 || cacheIdx != ns || cache.nextSplit >= 0 || !siText(cache)) return false;
+    if (!heapNoop(&raBound)) return false;
+    raIt = 0;
+    raMoved = 0;
+    raNs = ns;
+    return true;
+  }
+  // the loop top (:352-356) and the poll checks (:358-396) for the cached state: its next base, or -1
+  // when the run ends here
+  GWA_HD int raNext() {
+    if (raIt >= cfg.runAheadMax) return -1;
+    if (numFMIndexSearches > upperSearches || status == ST_OVERFLOW || status == ST_ERROR) return -1;
+    if (keyOfLocal(cache) >= raBound) return -1;
+    if ((((uint32_t)cache.state >> 24) & 3) != 0 || cRemaining(cache) == 0) return -1;
+    if ((cache.state & 0x1F) == 0x1F) return -1;
+    const int nm = (int)(((uint32_t)cache.state >> 8) & 0xFF);
+    if (nm > minMismatches) return -1;
+    const int ubs = stateScore(cache, 0, true);
+    if (ubs < 0 || ubs < bestScore) return -1;
+    if (!siText(cache)) return -1;
+    const int nb = qcode(cStrand(cache), cNextIdx(cache));
+    // (the parent's checked flag for nb is not recorded: the parent is never read again, and the
+    // child takes only the priority bits of the parent's state word)
+    if ((cache.state & (1 << nb)) != 0 || siIsEmpty(cache, nb)) return -1;
+    return nb;
+  }
+  // the run's end: its last state takes the place of the first (raNs, never referenced) in the queue;
+  // -2 overflow
+  GWA_HD int raFinish() {
+    if (!raMoved) return raNs;
     const int id = allocState();
     if (id < 0) return -2;
     cacheDirty = 0;
     cacheIdx = id;
     if (deferrable(cache)) cacheDirty = 1;
-    else L.arena()[id] = cache;
+    else { GWA_PW(PR_WA, PR_EA, sizeof(DState<R>)); L.arena()[id] = cache; }
     return id;
   }
 
@@ -2443,6 +2498,7 @@ struct BsfLane {
   }
   // AlignmentProcess.align (:210-268) after the search: pick the reported chains
   GWA_HD void writeSearchOutput(OutHeader *oh, const OutSlots &os, uint32_t rd_) {
+    GWA_PW(PR_WO, PR_EO, 16 * 4);
     oh->fmSearches = numFMIndexSearches;
     oh->searchBlocks = blocks;
     oh->saReads = saReads;
@@ -2490,6 +2546,7 @@ struct BsfLane {
         o.diff = h.diff; o.strand = h.strand; o.numHits = h.numHits; o.next = -1;
         o.cigarOff = ncg;
         o.cigarLen = (uint32_t)h.cigarLen;
+        GWA_PW(PR_WO, PR_EO, sizeof(OutHit) + 2 * h.cigarLen);
         for (int i = 0; i < h.cigarLen; ++i) oCig[ncg++] = L.cigar()[h.cigarOff + i];
         if (prevOut >= 0) oHits[prevOut].next = (int32_t)nh;
         prevOut = (int)nh;

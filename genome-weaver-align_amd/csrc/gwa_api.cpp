@@ -1053,10 +1053,16 @@ int gwa_batch_run(gwa_batch_t *b) {
         for (size_t i = 0; i < pv.size(); ++i) sum[i % PR_N] += (double)pv[i];
         static const char *nm[PR_N] = {"poll", "report", "runahead", "exp1", "add1", "expN", "split", "newstate",
                                        "verify", "nfa", "fm", "seed", "nVerifyWave", "nVerifyLane", "nStepWave",
-                                       "nStepLane", "dpFwd", "dpTrace", "sumWait", "wave"};
-        fprintf(stderr, "[gwa-prof] tier %d reads %u lanes %u (Gcycles summed over waves; counts in M):", t, n, lanes);
-        for (int q = 0; q < PR_N; ++q)
-          if (nm[q][0] != '-') fprintf(stderr, " %s=%.2f", nm[q], sum[q] / ((q >= PR_NVW && q <= PR_NSL) || q == PR_NWAIT ? 1e6 : 1e9));
+                                       "nStepLane", "dpFwd", "dpTrace", "sumWait", "nBuildWave", "nBuildLane",
+                                       "wArenaGB", "eArena", "wWordGB", "eWord", "wDpGB", "eDp", "eDpWave",
+                                       "wHitGB", "eHit", "wOutGB", "eOut", "-", "wave"};
+        fprintf(stderr, "[gwa-prof] tier %d reads %u lanes %u (Gcycles summed over waves; counts in M; bytes in GB):", t, n, lanes);
+        for (int q = 0; q < PR_N; ++q) {
+          if (nm[q][0] == '-') continue;
+          const bool count = (q >= PR_NVW && q <= PR_NSL) || q == PR_NWAIT || q == PR_NBW || q == PR_NBL ||
+                             (q >= PR_WA && q <= PR_EO && nm[q][0] == 'e');
+          fprintf(stderr, " %s=%.3f", nm[q], sum[q] / (count ? 1e6 : 1e9));
+        }
         fprintf(stderr, "\n");
       }
 #else

@@ -213,6 +213,14 @@ struct ScanRes {
 
 // CIGAR op = (len << 3) | type ; type: M0 I1 D2 N3 S4 H5 P6 X7  (A/CIGAR.java:39-47)
 // search-loop profiling regions (-DGWA_PROF builds)
-enum { PR_POLL, PR_REPORT, PR_BOUND, PR_EXP1, PR_ADD1, PR_EXPN, PR_SPLIT, PR_LOOP, PR_VERIFY, PR_NFA, PR_FM, PR_SEED, PR_NVW, PR_NVL, PR_NSW, PR_NSL, PR_DPF, PR_DPT, PR_NWAIT, PR_N = 20 };
+// (cycle regions, then wave / lane execution counts; PR_W* / PR_E*: bytes / lane store events of
+// each HBM store site of the search -- arena states, state words, DP history, hit/list/CIGAR/memo
+// slices, the output slots; PR_EDW: wave store instructions of the DP history)
+enum {
+  PR_POLL, PR_REPORT, PR_BOUND, PR_EXP1, PR_ADD1, PR_EXPN, PR_SPLIT, PR_LOOP, PR_VERIFY, PR_NFA, PR_FM, PR_SEED,
+  PR_NVW, PR_NVL, PR_NSW, PR_NSL, PR_DPF, PR_DPT, PR_NWAIT, PR_NBW, PR_NBL,
+  PR_WA, PR_EA, PR_WS, PR_ES, PR_WD, PR_ED, PR_EDW, PR_WH, PR_EH, PR_WO, PR_EO,
+  PR_N = 34
+};
 
 }  // namespace gwa

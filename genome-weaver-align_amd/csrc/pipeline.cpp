@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <zlib.h>
 
+#include "snappy_stream.h"
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -474,9 +476,18 @@ struct Run {
   }
 };
 
+// 1: gzip (.gz), 2: snappy-java (.snap, R/ReadReaderFactory.java:130-139), 0: plain
+int compressedKind(const char *path) {
+  const size_t n = strlen(path);
+  if (n > 3 && strcmp(path + n - 3, ".gz") == 0) return 1;
+  if (n > 5 && strcmp(path + n - 5, ".snap") == 0) return 2;
+  return 0;
+}
+
 int formatOf(const char *path) {
   std::string s(path);
   if (s.size() > 3 && s.compare(s.size() - 3, 3, ".gz") == 0) s.resize(s.size() - 3);
+  else if (s.size() > 5 && s.compare(s.size() - 5, 5, ".snap") == 0) s.resize(s.size() - 5);
   auto ends = [&](const char *x) {
     const size_t n = strlen(x);
     return s.size() >= n && s.compare(s.size() - n, n, x) == 0;
@@ -642,8 +653,8 @@ int gwa_reads_shard_range(const char *path, uint32_t shard, uint32_t nshards, ui
   try {
     if (nshards == 0 || shard >= nshards) throw std::runtime_error("shard index out of range");
     const int fmt = formatOf(path);
-    if (strlen(path) > 3 && strcmp(path + strlen(path) - 3, ".gz") == 0)
-      throw std::runtime_error(std::string("a sharded run needs an uncompressed read file (not .gz): ") + path);
+    if (compressedKind(path))
+      throw std::runtime_error(std::string("a sharded run needs an uncompressed read file (not .gz / .snap): ") + path);
     in = ::open(path, O_RDONLY);
     if (in < 0) throw std::runtime_error(std::string("cannot open ") + path);
     struct stat st;
@@ -674,16 +685,22 @@ int gwa_pipeline_align_file_range(gwa_pipeline_t *p, const char *path, int fd, u
   BufPool &pool = p->pool;
   Run run(p);
   gzFile f = nullptr;
+  std::unique_ptr<gwa::SnapReader> snap;
   int in = -1;
   try {
     const int fmt = formatOf(path);
-    const bool gz = strlen(path) > 3 && strcmp(path + strlen(path) - 3, ".gz") == 0;
+    const int ck = compressedKind(path);
+    const bool gz = ck != 0;  // (a compressed stream: gzip or snappy-java)
     const bool whole = begin == 0 && end == ~0ull;
     if (gz) {
       if (!whole) throw std::runtime_error(std::string("a byte range needs an uncompressed read file: ") + path);
-      f = gzopen(path, "rb");
-      if (!f) throw std::runtime_error(std::string("cannot open ") + path);
-      gzbuffer(f, 1u << 20);
+      if (ck == 1) {
+        f = gzopen(path, "rb");
+        if (!f) throw std::runtime_error(std::string("cannot open ") + path);
+        gzbuffer(f, 1u << 20);
+      } else {
+        snap.reset(new gwa::SnapReader(path));
+      }
     } else {
       in = ::open(path, O_RDONLY);
       if (in < 0) throw std::runtime_error(std::string("cannot open ") + path);
@@ -770,7 +787,9 @@ int gwa_pipeline_align_file_range(gwa_pipeline_t *p, const char *path, int fd, u
           c.buf = pool.get(reserve + chunk);
           const auto r0 = Clock::now();
           char *dst = c.buf->p + reserve;
-          if (gz) {
+          if (snap) {
+            c.got = snap->read(dst, chunk);
+          } else if (gz) {
             while (c.got < chunk) {
               const int r = gzread(f, dst + c.got, (unsigned)(chunk - c.got));
               if (r < 0) throw std::runtime_error(std::string("read error: ") + path);

@@ -75,6 +75,17 @@ def shard_range(path, shard, nshards):
     return b.value, e.value
 
 
+def snappy_decompress(data):
+    """The bytes of a `.snap` file (R/ReadReaderFactory.java:130-139, snappy-java SnappyInputStream),
+    decompressed by the library (include/gwa.h gwa_snappy_decompress; host only)."""
+    out, n = ctypes.c_void_p(), ctypes.c_uint64()
+    _check(lib().gwa_snappy_decompress(data, len(data), ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        lib().gwa_free(out)
+
+
 class PipelineStats(ctypes.Structure):
     _fields_ = [("reads", ctypes.c_uint64), ("batches", ctypes.c_uint64), ("wall_s", ctypes.c_double),
                 ("read_s", ctypes.c_double), ("device_kernel_s", ctypes.c_double * 16), ("parse_s", ctypes.c_double),
@@ -93,7 +104,7 @@ EXPORTS = ["gwa_config_default", "gwa_last_error", "gwa_device_count", "gwa_inde
            "gwa_batch_sam_copy",
            "gwa_pipeline_open", "gwa_pipeline_align", "gwa_pipeline_align_file", "gwa_pipeline_align_file_range",
            "gwa_reads_shard_range", "gwa_pipeline_stats",
-           "gwa_pipeline_close", "gwa_reads_parse", "gwa_reads_free"]
+           "gwa_pipeline_close", "gwa_reads_parse", "gwa_reads_free", "gwa_snappy_decompress"]
 
 
 def lib():
@@ -141,6 +152,7 @@ def lib():
         L.gwa_reads_shard_range.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, P(U64), P(U64)]
         L.gwa_pipeline_stats.argtypes = [V, P(PipelineStats)]
         L.gwa_pipeline_close.argtypes = [V]
+        L.gwa_snappy_decompress.argtypes = [ctypes.c_char_p, U64, P(V), P(U64)]
         _lib = L
     return _lib
 

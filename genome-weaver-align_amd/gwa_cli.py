@@ -2,7 +2,7 @@
 A/AlignmentConfig.java:40-72, A/AlignmentScoreConfig.java:37-77).
 
   python genome-weaver-align_amd/gwa_cli.py bwt ref.fa            (writes ref.fa.gwa.idx)
-  python genome-weaver-align_amd/gwa_cli.py align -r ref.fa [-q SEQ | reads.fq[.gz] | reads.fa[.gz]]
+  python genome-weaver-align_amd/gwa_cli.py align -r ref.fa [-q SEQ | reads.fq[.gz|.snap] | reads.fa[.gz|.snap]]
          [-k 0.1] [-m bsf|sf|bd|bwa] [-R besthit|allhits|topL] [-L 5] [-g 1] [-e 4] [-s 1] [-M 1] [-N 3]
          [-G 11] [-E 4] [-S 11] [-P 5] [-W 31] [--silent] [--devices 0,1,..] [--batch 1048576]
 
@@ -15,7 +15,7 @@ files its `bwt` command wrote next to the FASTA (A/FMIndexOnGenome.java:60-86, A
 from the FASTA.
 
 Read input follows ReadReaderFactory.createReader (R/ReadReaderFactory.java:126-151): `.fa`,
-`.fasta`, `.fan`, `.fastq`, `.fq`, optionally `.gz`; `-q` aligns one query named "read" with no
+`.fasta`, `.fan`, `.fastq`, `.fq`, optionally `.gz` or `.snap` (snappy-java stream); `-q` aligns one query named "read" with no
 qualities (R/ReadReaderFactory.java:167-180).  Read names are the first whitespace-delimited token
 of the header line (utgb FastqReader / FASTAPullParser are unvendored: parity unpinned).
 """
@@ -33,11 +33,21 @@ import gwa  # noqa: E402
 
 
 def _open(path):
+    if path.endswith(".snap"):  # snappy-java stream (R/ReadReaderFactory.java:130-139)
+        with open(path, "rb") as f:
+            return io.TextIOWrapper(io.BytesIO(gwa.snappy_decompress(f.read())))
     return gzip.open(path, "rt") if path.endswith(".gz") else open(path, "rt")
 
 
+def _open_bytes(path):
+    if path.endswith(".snap"):
+        with open(path, "rb") as f:
+            return io.BytesIO(gwa.snappy_decompress(f.read()))
+    return gzip.open(path, "rb") if path.endswith(".gz") else open(path, "rb")
+
+
 def _kind(path):
-    p = path[:-3] if path.endswith(".gz") else path
+    p = path[:-3] if path.endswith(".gz") else path[:-5] if path.endswith(".snap") else path
     if p.endswith((".fa", ".fasta", ".fan")):
         return "fasta"
     if p.endswith((".fastq", ".fq")):
@@ -268,8 +278,7 @@ def align_pairs(ns, fm, cfg, w):
     if cfg.strategy.lower() != "bsf":
         raise gwa.GwaError("paired-end alignment runs -m bsf")
     pe = gwa.PairedEndAligner(fm, cfg, ns.insert_min, ns.insert_max)
-    opener = [gzip.open if f.endswith(".gz") else open for f in ns.readFiles]
-    with opener[0](ns.readFiles[0], "rb") as f1, opener[1](ns.readFiles[1], "rb") as f2:
+    with _open_bytes(ns.readFiles[0]) as f1, _open_bytes(ns.readFiles[1]) as f2:
         p1 = gwa.ParsedReads(f1.read(), _kind(ns.readFiles[0]))
         p2 = gwa.ParsedReads(f2.read(), _kind(ns.readFiles[1]))
     try:

@@ -233,11 +233,11 @@ int gwa_pipeline_open(gwa_index_t *const *ix, int n_ix, const gwa_config_t *cfg,
                       int workers_per_device, gwa_pipeline_t **out);
 /* SAM (no header) of any number of reads, in input order. */
 int gwa_pipeline_align(gwa_pipeline_t *p, const gwa_reads_t *reads, gwa_results_t *out);
-/* A FASTA / FASTQ file (.fa .fasta .fan .fastq .fq, optionally .gz; ReadReaderFactory.createReader,
+/* A FASTA / FASTQ file (.fa .fasta .fan .fastq .fq, optionally .gz or .snap; ReadReaderFactory.createReader,
  * R/ReadReaderFactory.java:126-151) streamed through the devices; SAM records (no header) are
  * written to fd in input order.  *n_reads = reads aligned. */
 int gwa_pipeline_align_file(gwa_pipeline_t *p, const char *path, int fd, uint64_t *n_reads);
-/* The same over the bytes [begin, end) of a plain (not .gz) read file, which must start at a record
+/* The same over the bytes [begin, end) of a plain (not .gz / .snap) read file, which must start at a record
  * (gwa_reads_shard_range gives such ranges). */
 int gwa_pipeline_align_file_range(gwa_pipeline_t *p, const char *path, int fd, uint64_t begin, uint64_t end,
                                   uint64_t *n_reads);
@@ -246,6 +246,10 @@ int gwa_pipeline_align_file_range(gwa_pipeline_t *p, const char *path, int fd, u
  * file, cut at record starts, so that the shards' SAM files concatenated in shard order equal a
  * one-process run's (the header belongs to shard 0). */
 int gwa_reads_shard_range(const char *path, uint32_t shard, uint32_t nshards, uint64_t *begin, uint64_t *end);
+/* The bytes of a `.snap` file (R/ReadReaderFactory.java:130-139, org.xerial.snappy.SnappyInputStream):
+ * a snappy-java stream (magic header, then length-prefixed Snappy blocks) or one bare Snappy block,
+ * decompressed into *out (malloc'd, NUL-terminated; gwa_free).  Host only, no device needed. */
+int gwa_snappy_decompress(const uint8_t *in, uint64_t n, char **out, uint64_t *out_len);
 int gwa_pipeline_stats(const gwa_pipeline_t *p, gwa_pipeline_stats_t *st);
 void gwa_pipeline_close(gwa_pipeline_t *p);
 

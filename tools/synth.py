@@ -313,6 +313,64 @@ def to_strings(seqs):
     return [SYM[row].tobytes().decode() for row in seqs]
 
 
+_TO3BIT = np.full(256, 4, dtype=np.uint8)
+for _c, _v in ((b"Aa", 0), (b"Cc", 1), (b"Gg", 2), (b"TtUu", 3)):
+    for _b in _c:
+        _TO3BIT[_b] = _v
+
+
+def fasta_codes(path):
+    """A FASTA file (e.g. $GWA_HG19) as (codes, names, lengths), the same values the library's packFasta
+    (genome-weaver-align_amd/csrc/host_index.cpp; A/PackFasta.java:81-108) gives: every sequence line
+    trimmed of bytes <= ' ' at both ends and each byte through to3bit (A/ACGT.java:36-43), the contig
+    name the first token of its '>' line (up to whitespace or '|').  Vectorised over the whole file."""
+    raw = np.fromfile(path, dtype=np.uint8)
+    nl = np.flatnonzero(raw == 10)
+    starts = np.concatenate([[0], nl + 1])
+    ends = np.concatenate([nl, [raw.size]])
+    keep = starts < ends
+    starts, ends = starts[keep], ends[keep]
+    hdr = raw[starts] == ord(">")
+    names, seq_parts, lengths = [], [], []
+    hidx = np.flatnonzero(hdr)
+    for j, h in enumerate(hidx):
+        s, e = int(starts[h]) + 1, int(ends[h])
+        line = raw[s:e].tobytes().rstrip(b"\r").decode("latin-1")
+        tok = line.strip().split()[0] if line.strip() else ""
+        names.append(tok.split("|")[0])
+        lo = int(ends[h]) + 1
+        hi = int(starts[hidx[j + 1]]) if j + 1 < len(hidx) else raw.size
+        block = raw[lo:hi]
+        ws = block <= 32
+        cr = np.flatnonzero(block == 13)
+        if np.count_nonzero(ws) == np.count_nonzero(block == 10) + cr.size and \
+                np.all((cr + 1 >= block.size) | (block[np.minimum(cr + 1, block.size - 1)] == 10)):
+            # the usual file: the only bytes <= ' ' are line ends ("\n", "\r\n")
+            seq = _TO3BIT[block[~ws]]
+            seq_parts.append(seq)
+            lengths.append(int(seq.size))
+            continue
+        # per line: drop bytes <= ' ' (the newline too) that lead or trail the line
+        lid = np.cumsum(block == 10) - (block == 10)  # line index of every byte (a newline ends its line)
+        solid = ~ws
+        # first / last solid byte position of each line
+        nlines = int(lid[-1]) + 1 if block.size else 0
+        first = np.full(nlines, block.size, dtype=np.int64)
+        last = np.full(nlines, -1, dtype=np.int64)
+        pos = np.flatnonzero(solid)
+        if pos.size:
+            np.minimum.at(first, lid[pos], pos)
+            np.maximum.at(last, lid[pos], pos)
+        idx = np.arange(block.size)
+        inner = (idx >= first[lid]) & (idx <= last[lid]) if block.size else np.zeros(0, bool)
+        del ws, solid, pos, idx
+        seq = _TO3BIT[block[inner]]
+        seq_parts.append(seq)
+        lengths.append(int(seq.size))
+    codes = np.concatenate(seq_parts) if seq_parts else np.zeros(0, np.uint8)
+    return codes, names, lengths
+
+
 def fasta_text(codes, names, lengths, width=60):
     parts = []
     off = 0
