@@ -78,13 +78,59 @@ struct gwa_index {
   int32_t starKey = -3, emptyKey = -2;  // name keys of "*" and "" (SamText)
   size_t bytes = 0;
   IndexView view{};
-  // reusable search scratch: one batch at a time runs its kernels on the index (runMu); batch set-up
-  // (H2D) and results (D2H, SAM) run outside the lock on each batch's own stream, so several host
-  // threads can keep one device busy (gwa_pipeline)
-  uint8_t *scratch = nullptr;
-  size_t scratchBytes = 0;
-  std::mutex runMu;
+  // Search scratch buffers, reused across batches: a running batch takes one from the pool and puts
+  // it back after its tiers, so batches of several host threads run their kernels concurrently on
+  // the device (each on its own stream and scratch; gwa_pipeline), one buffer per concurrent batch.
+  std::mutex scratchMu;
+  std::vector<std::pair<uint8_t *, size_t>> scratchFree;
+  size_t scratchHeld = 0;  // bytes of every buffer, in the pool or taken
 };
+
+namespace {
+// a scratch buffer of the index's pool for the duration of one gwa_batch_run
+struct Scratch {
+  gwa_index *ix;
+  hipStream_t s;  // the batch's stream: drained before the buffer goes back to the pool
+  uint8_t *p = nullptr;
+  size_t bytes = 0;
+  Scratch(gwa_index *x, hipStream_t st) : ix(x), s(st) {
+    std::lock_guard<std::mutex> g(ix->scratchMu);
+    if (!ix->scratchFree.empty()) {  // the largest free one
+      size_t best = 0;
+      for (size_t i = 1; i < ix->scratchFree.size(); ++i)
+        if (ix->scratchFree[i].second > ix->scratchFree[best].second) best = i;
+      p = ix->scratchFree[best].first;
+      bytes = ix->scratchFree[best].second;
+      ix->scratchFree.erase(ix->scratchFree.begin() + (long)best);
+    }
+  }
+  // at least `need` bytes (the old contents are not kept)
+  void ensure(size_t need) {
+    if (need <= bytes) return;
+    release();
+    HIPCHK(hipMalloc(&p, need));
+    bytes = need;
+    std::lock_guard<std::mutex> g(ix->scratchMu);
+    ix->scratchHeld += need;
+  }
+  // give the memory back to the device (a grown tier's tens of GiB for a few reads)
+  void release() {
+    if (!p) return;
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(p);
+    std::lock_guard<std::mutex> g(ix->scratchMu);
+    ix->scratchHeld -= bytes;
+    p = nullptr;
+    bytes = 0;
+  }
+  ~Scratch() {
+    if (!p) return;
+    (void)hipStreamSynchronize(s);  // (an error path may leave a kernel of this batch running)
+    std::lock_guard<std::mutex> g(ix->scratchMu);
+    ix->scratchFree.push_back({p, bytes});
+  }
+};
+}  // namespace
 
 struct gwa_batch {
   gwa_index *ix = nullptr;
@@ -158,7 +204,8 @@ static void freeIndexDev(gwa_index *ix) {
   if (ix->d_chrRank) (void)hipFree(ix->d_chrRank);
   if (ix->d_ctg) (void)hipFree(ix->d_ctg);
   if (ix->d_ctgOff) (void)hipFree(ix->d_ctgOff);
-  if (ix->scratch) (void)hipFree(ix->scratch);
+  for (auto &f : ix->scratchFree) (void)hipFree(f.first);
+  ix->scratchFree.clear();
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
 }
 
@@ -795,12 +842,12 @@ static uint32_t tierValue(const char *var, int t, uint32_t def) {
   return v > 0 ? (uint32_t)v : def;
 }
 
-// Search scratch the tiers may hold: half of what is free on the device plus what the index's
-// scratch already holds, at most 64 GiB (the index replica and the batches keep the rest).
-static uint64_t scratchBudget(const gwa_index *ix) {
+// Search scratch one batch's tiers may hold: half of what is free on the device plus the buffer the
+// batch already holds, at most 64 GiB (the index replica and the other batches keep the rest).
+static uint64_t scratchBudget(size_t held) {
   size_t freeB = 0, totalB = 0;
   if (hipMemGetInfo(&freeB, &totalB) != hipSuccess) return 16ull << 30;
-  return std::min<uint64_t>(64ull << 30, ((uint64_t)freeB + ix->scratchBytes) / 2);
+  return std::min<uint64_t>(64ull << 30, ((uint64_t)freeB + held) / 2);
 }
 
 // the batch's output slots + pool (gwa_layout.h OutSlots); pool counters at d_count[12..14]
@@ -861,7 +908,6 @@ int gwa_batch_run(gwa_batch_t *b) {
     gwa_index *ix = b->ix;
     HIPCHK(hipSetDevice(ix->device));
     hipStream_t s = b->stream;
-    std::lock_guard<std::mutex> runLock(ix->runMu);
     memset(&b->stats, 0, sizeof(b->stats));
     if (b->headerOnly) {
       b->ran = true;
@@ -871,6 +917,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     b->poolUsedH = b->poolUsedC = 0;
     b->deep.clear();
     ReadsView rv{b->d_codes, b->d_off, b->d_len, b->n};
+    Scratch scr(ix, s);  // this run's search scratch (from the index's pool, back to it at the end)
     Events ev;
     hipEvent_t e0 = ev.e[0], e1 = ev.e[1], e2 = ev.e[2];
     // encode the read text in HBM (ACGTSequence(String), A/ACGTSequence.java:86-97): lengths and
@@ -966,7 +1013,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     };
     while (n > 0) {
       if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
-      const uint64_t budget = scratchBudget(ix);
+      const uint64_t budget = scratchBudget(scr.bytes);
       // Few reads left after the first tier: straight to the largest tier whose capacities give every
       // one of them a slice within the scratch budget.  A rerun restarts a search from its seeds, and
       // the reads still overflowing here are the heaviest (C4 -m bsf: 5k reads in tier 2, of which 2
@@ -1021,14 +1068,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       // a very sparse tier whose lanes fit one round of one workgroup per CU (256 CUs x 4 waves):
       // its queue tops go to LDS (bsf_search_kernel LH 2; the 64 KiB array leaves one workgroup per CU)
       const bool deepLds = !sf && tb > 0 && caps.sparse >= 8 && lanes <= 65536u;
-      const size_t need = (size_t)mem(stride, lanes, spUsed);
-      if (need > ix->scratchBytes) {
-        if (ix->scratch) HIPCHK(hipFree(ix->scratch));
-        ix->scratch = nullptr;
-        ix->scratchBytes = 0;
-        HIPCHK(hipMalloc(&ix->scratch, need));
-        ix->scratchBytes = need;
-      }
+      scr.ensure((size_t)mem(stride, lanes, spUsed));
       uint32_t *ovfCount = b->d_count + 1 + tb;
       uint32_t *ovfBits = b->d_count + 15;
       HIPCHK(hipMemsetAsync(ovfCount, 0, 4, s));
@@ -1042,7 +1082,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
       launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
-                   ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount,
+                   scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount,
                    ovfBits, s, (uint32_t *)d_prof, -1);
       {
         std::vector<uint64_t> pv((size_t)lanes * PR_N);
@@ -1068,11 +1108,11 @@ int gwa_batch_run(gwa_batch_t *b) {
 #else
       if (sf)
         launchSfSearch(b->R, qwFor(b->maxM), b->sfWrap, lanes, ix->view, b->scfg, b->st, rv,
-                       (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, ix->scratch, stride, caps, b->d_oh, os,
+                       (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s);
       else
         launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
-                     ix->scratch, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1],
+                     scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1],
                      ovfCount, ovfBits, s);
 #endif
       HIPCHK(hipGetLastError());
@@ -1153,19 +1193,12 @@ int gwa_batch_run(gwa_batch_t *b) {
       const uint64_t stride = laneBytesFor(4, rc);
       uint32_t lanes = std::min<uint32_t>(b->pairs, 65536u);
       lanes = (lanes + 63) / 64 * 64;
-      const size_t need = (size_t)(stride + ilvBytesFor(rc)) * lanes;
-      if (need > ix->scratchBytes) {
-        if (ix->scratch) HIPCHK(hipFree(ix->scratch));
-        ix->scratch = nullptr;
-        ix->scratchBytes = 0;
-        HIPCHK(hipMalloc(&ix->scratch, need));
-        ix->scratchBytes = need;
-      }
+      scr.ensure((size_t)(stride + ilvBytesFor(rc)) * lanes);
       uint32_t *heavyCount = b->d_heavy + b->pairs;
       HIPCHK(hipEventRecord(e1, s));
       HIPCHK(hipMemsetAsync(heavyCount, 0, 8, s));
       launchPairRescue(lanes, ix->view, b->scfg, b->st, rv, samText(b), b->d_oh, b->d_hits, b->d_cig, b->pairs, b->minIns,
-                       b->maxIns, ix->scratch, stride, rc, b->d_rescue,
+                       b->maxIns, scr.p, stride, rc, b->d_rescue,
                        getenv("GWA_PAIR_QUAD") ? atol(getenv("GWA_PAIR_QUAD")) : kPairQuad, b->d_heavy, heavyCount, s);
       HIPCHK(hipGetLastError());
       uint32_t hc[2] = {0, 0};
@@ -1190,9 +1223,7 @@ int gwa_batch_run(gwa_batch_t *b) {
     // than hold it for the index's life (the next batch allocates what its tiers need)
     if (t > kNumTiers) {
       HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipFree(ix->scratch));
-      ix->scratch = nullptr;
-      ix->scratchBytes = 0;
+      scr.release();
     }
     b->ran = true;
     return 0;

@@ -9,9 +9,10 @@
 //
 // Threads: one reader (the file: framing of complete records only, no parsing), W workers per
 // device (parse a framed slice, set the batch up on the device, run the kernels, format the SAM),
-// and the caller, which writes the results in batch order.  With two workers per device, one
-// worker's set-up and SAM formatting overlap the other's kernels (gwa_index serialises the kernels
-// of its batches, gwa_api.cpp runMu).  At most `depth` batches are in flight, which bounds memory.
+// and the caller, which writes the results in batch order.  The workers of one device run their
+// batches' kernels concurrently, each batch on its own stream and search scratch (gwa_api.cpp
+// Scratch), so one batch's set-up, deep-tier tail and SAM formatting overlap another's kernels.  At
+// most `depth` batches are in flight, which bounds memory.
 #include <hip/hip_runtime.h>
 #include <zlib.h>
 
