@@ -10,10 +10,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "bsf_core.h"
@@ -51,6 +53,113 @@ T *devUpload(const std::vector<T> &v, hipStream_t s, size_t *acc) {
   T *p = devAlloc<T>(v.size(), acc);
   if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
   return p;
+}
+
+// Device memory and streams of batches, kept per device for reuse: a pipeline creates and frees one
+// batch per chunk of a read file, and hipFree / hipStreamDestroy wait for the whole device, so each
+// free would stall the kernels other host threads' batches have in flight.  A freed buffer goes back
+// only after the stream that used it is drained (that stream alone).
+struct DevCache {
+  std::mutex mu;
+  std::multimap<size_t, void *> free;         // cached blocks by size
+  std::unordered_map<void *, size_t> size;    // every block handed out or cached -> its size
+  std::vector<hipStream_t> streams;           // idle streams
+  size_t cached = 0;
+};
+DevCache g_devCache[64];
+const size_t kDevCacheCap = (size_t)24 << 30;  // cached bytes per device at most
+
+DevCache &devCache() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return g_devCache[d & 63];
+}
+size_t cacheRound(size_t b) {
+  b = std::max<size_t>(b, 256);
+  int e = 63 - __builtin_clzll(b);
+  const size_t step = std::max<size_t>(256, ((size_t)1 << e) / 8);
+  return (b + step - 1) / step * step;
+}
+void *batchMalloc(size_t bytes) {
+  DevCache &c = devCache();
+  const size_t r = cacheRound(bytes);
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.free.lower_bound(r);
+    if (it != c.free.end() && it->first <= r + r / 4) {
+      void *p = it->second;
+      c.cached -= it->first;
+      c.free.erase(it);
+      return p;
+    }
+  }
+  void *p = nullptr;
+  if (hipMalloc(&p, r) != hipSuccess) {  // give the cached blocks back and try once more
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> g(c.mu);
+    for (auto &kv : c.free) {
+      (void)hipFree(kv.second);
+      c.size.erase(kv.second);
+    }
+    c.free.clear();
+    c.cached = 0;
+    HIPCHK(hipMalloc(&p, r));
+  }
+  std::lock_guard<std::mutex> g(c.mu);
+  c.size[p] = r;
+  return p;
+}
+// p back to the cache once stream s (the last user of p; nullptr: none pending) has drained
+void batchFree(void *p, hipStream_t s) {
+  if (!p) return;
+  if (s) (void)hipStreamSynchronize(s);
+  DevCache &c = devCache();
+  std::unique_lock<std::mutex> g(c.mu);
+  auto it = c.size.find(p);
+  if (it == c.size.end()) {  // (not a cached block)
+    g.unlock();
+    (void)hipFree(p);
+    return;
+  }
+  if (c.cached + it->second > kDevCacheCap) {
+    c.size.erase(it);
+    g.unlock();
+    (void)hipFree(p);
+    return;
+  }
+  c.cached += it->second;
+  c.free.insert({it->second, p});
+}
+template <class T>
+T *bAlloc(size_t n) {
+  return (T *)batchMalloc(std::max<size_t>(n * sizeof(T), 64));
+}
+template <class T>
+T *bUpload(const std::vector<T> &v, hipStream_t s) {
+  T *p = bAlloc<T>(v.size());
+  if (!v.empty()) HIPCHK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  return p;
+}
+hipStream_t batchStream() {
+  DevCache &c = devCache();
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    if (!c.streams.empty()) {
+      hipStream_t s = c.streams.back();
+      c.streams.pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return s;
+}
+void batchStreamDone(hipStream_t s) {
+  if (!s) return;
+  (void)hipStreamSynchronize(s);
+  DevCache &c = devCache();
+  std::lock_guard<std::mutex> g(c.mu);
+  c.streams.push_back(s);
 }
 
 int fail(const std::string &m) {
@@ -544,16 +653,16 @@ static void freeBatchDev(gwa_batch *b) {
                 b->d_stair, b->d_stairBase, b->d_stairBad, b->d_fieldOwn[0], b->d_fieldOwn[1], b->d_fieldOwn[2],
                 b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtErr, b->d_fmtTmp, b->d_fmtText, b->d_stats,
                 b->d_row, b->d_seen, b->d_encTmp, b->d_qualNull, b->d_rescue, b->d_heavy};
-  for (void *p : ps)
-    if (p) (void)hipFree(p);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);  // (then every buffer below is idle)
+  for (void *p : ps) batchFree(p, nullptr);
   // the text blobs (one allocation may back several of them)
   char *tx[3] = {b->d_seqText, b->d_nameText, b->d_qualText};
   for (int i = 0; i < 3; ++i) {
     bool dup = false;
     for (int j = 0; j < i; ++j) dup = dup || tx[j] == tx[i];
-    if (tx[i] && !dup) (void)hipFree(tx[i]);
+    if (tx[i] && !dup) batchFree(tx[i], nullptr);
   }
-  if (b->stream) (void)hipStreamDestroy(b->stream);
+  batchStreamDone(b->stream);
   b->stream = nullptr;
 }
 
@@ -584,7 +693,7 @@ static bool batchHead(gwa_index *ix, const gwa_config_t *cfg, uint32_t n, gwa_ba
   sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
   sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
   sc.textCache = getenv("GWA_TEXT_CACHE") ? atoi(getenv("GWA_TEXT_CACHE")) : 0;
-  HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  b->stream = batchStream();
   return false;
 }
 
@@ -597,13 +706,13 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   hipStream_t s = b->stream;
   const uint64_t codeBound = seqBytes + 16ull * n + 32;
   if (codeBound > 0xFFFFFFFFull) throw std::runtime_error("read batch too large (> 4 GiB of codes): use fewer reads per batch");
-  b->d_codes = devAlloc<uint8_t>(codeBound);
-  b->d_off = devAlloc<uint32_t>((size_t)n + 1);
-  b->d_len = devAlloc<uint32_t>((size_t)n + 1);
-  b->d_row = devAlloc<uint32_t>((size_t)n + 1);
-  b->d_seen = devAlloc<uint32_t>(kLenSeen);
+  b->d_codes = bAlloc<uint8_t>(codeBound);
+  b->d_off = bAlloc<uint32_t>((size_t)n + 1);
+  b->d_len = bAlloc<uint32_t>((size_t)n + 1);
+  b->d_row = bAlloc<uint32_t>((size_t)n + 1);
+  b->d_seen = bAlloc<uint32_t>(kLenSeen);
   b->encTmpBytes = encodeScanTempBytes(n);
-  b->d_encTmp = devAlloc<uint8_t>(b->encTmpBytes);
+  b->d_encTmp = bAlloc<uint8_t>(b->encTmpBytes);
   // the length pass (read lengths, code offsets, the lengths present); gwa_batch_run encodes
   std::vector<uint32_t> seen(kLenSeen);
   HIPCHK(hipMemsetAsync(b->d_seen, 0, kLenSeen * sizeof(uint32_t), s));
@@ -650,9 +759,9 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   std::vector<uint64_t> tab, bad;
   std::vector<uint32_t> base;
   buildStairTables(lens, std::max(b->kmax, 0), tab, base, bad);
-  b->d_stair = devUpload(tab, s, nullptr);
-  b->d_stairBase = devUpload(base, s, nullptr);
-  b->d_stairBad = devUpload(bad, s, nullptr);
+  b->d_stair = bUpload(tab, s);
+  b->d_stairBase = bUpload(base, s);
+  b->d_stairBad = bUpload(bad, s);
   b->st.tab = b->d_stair;
   b->st.base = b->d_stairBase;
   b->st.bad = b->d_stairBad;
@@ -679,17 +788,17 @@ static void batchTail(gwa_batch *b, uint64_t seqBytes) {
   }
   if ((uint64_t)n * b->cigCap + b->poolCig >= 0xFFFFFFFFull)
     throw std::runtime_error("read batch too large for 32-bit output offsets: use fewer reads per batch");
-  b->d_sres = devAlloc<ScanRes>(n);
-  b->d_oh = devAlloc<OutHeader>(n);
-  b->d_hits = devAlloc<OutHit>((size_t)n * b->hitCap + b->poolHits);
-  b->d_cig = devAlloc<uint16_t>((size_t)n * b->cigCap + b->poolCig);
-  b->d_list[0] = devAlloc<uint32_t>(n);
-  b->d_list[1] = devAlloc<uint32_t>(n);
-  b->d_count = devAlloc<uint32_t>(16);
+  b->d_sres = bAlloc<ScanRes>(n);
+  b->d_oh = bAlloc<OutHeader>(n);
+  b->d_hits = bAlloc<OutHit>((size_t)n * b->hitCap + b->poolHits);
+  b->d_cig = bAlloc<uint16_t>((size_t)n * b->cigCap + b->poolCig);
+  b->d_list[0] = bAlloc<uint32_t>(n);
+  b->d_list[1] = bAlloc<uint32_t>(n);
+  b->d_count = bAlloc<uint32_t>(16);
   if (cfg->strategy == 1) {
     std::vector<uint32_t> all(n);
     for (uint32_t i = 0; i < n; ++i) all[i] = i;
-    b->d_all = devUpload(all, s, nullptr);
+    b->d_all = bUpload(all, s);
   }
   HIPCHK(hipStreamSynchronize(s));
 }
@@ -711,9 +820,9 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
       std::vector<uint64_t> o(off, off + n + 1);
       const uint64_t o0 = o[0];
       for (auto &x : o) x -= o0;
-      *dText = devAlloc<char>(o[n] + 32);  // (+32: the device reads the text in aligned 16-B chunks)
+      *dText = bAlloc<char>(o[n] + 32);  // (+32: the device reads the text in aligned 16-B chunks)
       if (o[n]) HIPCHK(hipMemcpyAsync(*dText, base + o0, o[n], hipMemcpyHostToDevice, s));
-      *dOff = devUpload(o, s, nullptr);
+      *dOff = bUpload(o, s);
       HIPCHK(hipStreamSynchronize(s));  // (o is a local vector)
       return o[n];
     };
@@ -732,7 +841,7 @@ int gwa_batch_create(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_reads_t
       b->d_qualB = off;
       b->d_qualE = off + 1;
       if (reads->qual_null) {  // reads without a quality among reads with one
-        b->d_qualNull = devAlloc<uint8_t>(n);
+        b->d_qualNull = bAlloc<uint8_t>(n);
         if (n) HIPCHK(hipMemcpyAsync(b->d_qualNull, reads->qual_null, n, hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
       }
@@ -764,21 +873,21 @@ int batchCreateFastq(gwa_index_t *ix, const gwa_config_t *cfg, const char *text,
     }
     b->hasQual = true;
     hipStream_t s = b->stream;
-    char *dText = devAlloc<char>(len + 32);  // (+32: the device reads the text in aligned 16-B chunks)
+    char *dText = bAlloc<char>(len + 32);  // (+32: the device reads the text in aligned 16-B chunks)
     b->d_seqText = dText;
     HIPCHK(hipMemcpyAsync(dText, text, len, hipMemcpyHostToDevice, s));
-    uint64_t *dStart = devAlloc<uint64_t>(n);
+    uint64_t *dStart = bAlloc<uint64_t>(n);
     HIPCHK(hipMemcpyAsync(dStart, start, (size_t)n * 8, hipMemcpyHostToDevice, s));
-    uint64_t *f = devAlloc<uint64_t>(6 * (size_t)n);
+    uint64_t *f = bAlloc<uint64_t>(6 * (size_t)n);
     b->d_fieldOwn[0] = f;
-    uint32_t *dErr = devAlloc<uint32_t>(1);
+    uint32_t *dErr = bAlloc<uint32_t>(1);
     uint32_t err = 0;
     HIPCHK(hipMemsetAsync(dErr, 0xFF, 4, s));
     launchFastqFields(dText, len, dStart, n, f, dErr, s);
     HIPCHK(hipMemcpyAsync(&err, dErr, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    (void)hipFree(dStart);
-    (void)hipFree(dErr);
+    batchFree(dStart, nullptr);  // (the stream was synchronised above)
+    batchFree(dErr, nullptr);
     if (err != 0xFFFFFFFFu) {  // the host parser words the error
       gwa_read_buf_t pb{};
       uint64_t used = 0;
@@ -872,13 +981,13 @@ static void growPool(gwa_batch *b, uint64_t usedH, uint64_t usedC, hipStream_t s
   const uint64_t fh = (uint64_t)b->n * b->hitCap, fc = (uint64_t)b->n * b->cigCap;
   if (fc + nc >= 0xFFFFFFFFull || fh + nh >= 0xFFFFFFFFull)
     throw std::runtime_error("reported hits exceed the 32-bit output offsets: use fewer reads per batch");
-  OutHit *h = devAlloc<OutHit>(fh + nh);
-  uint16_t *c = devAlloc<uint16_t>(fc + nc);
+  OutHit *h = bAlloc<OutHit>(fh + nh);
+  uint16_t *c = bAlloc<uint16_t>(fc + nc);
   HIPCHK(hipMemcpyAsync(h, b->d_hits, (fh + b->poolHits) * sizeof(OutHit), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(c, b->d_cig, (fc + b->poolCig) * sizeof(uint16_t), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
-  (void)hipFree(b->d_hits);
-  (void)hipFree(b->d_cig);
+  batchFree(b->d_hits, nullptr);  // (the stream was synchronised above)
+  batchFree(b->d_cig, nullptr);
   b->d_hits = h;
   b->d_cig = c;
   b->poolHits = nh;
@@ -1239,7 +1348,7 @@ static void ensureStats(gwa_batch *b) {
   if (b->statsDone || b->headerOnly || !b->ran) return;
   HIPCHK(hipSetDevice(b->ix->device));
   hipStream_t s = b->stream;
-  if (!b->d_stats) b->d_stats = devAlloc<unsigned long long>(kStatFields);
+  if (!b->d_stats) b->d_stats = bAlloc<unsigned long long>(kStatFields);
   launchStats(b->d_oh, b->n, b->d_stats, s);
   unsigned long long v[kStatFields];
   HIPCHK(hipMemcpyAsync(v, b->d_stats, sizeof(v), hipMemcpyDeviceToHost, s));
@@ -1284,11 +1393,11 @@ static SamText samText(const gwa_batch *b) {
 }
 
 template <class T>
-static void growDev(T **p, size_t *cap, size_t need) {
+static void growDev(T **p, size_t *cap, size_t need, hipStream_t s) {
   if (*p && *cap >= need) return;
-  if (*p) HIPCHK(hipFree(*p));
+  batchFree(*p, s);
   *p = nullptr;
-  *p = devAlloc<T>(need);
+  *p = bAlloc<T>(need);
   *cap = need;
 }
 
@@ -1301,19 +1410,18 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
   hipStream_t s = b->stream;
   if (!b->d_fmtLen || b->fmtCap < (size_t)n + 1) {
     void *ps[] = {b->d_fmtLen, b->d_fmtOff, b->d_fmtIdx, b->d_fmtTmp};
-    for (void *p : ps)
-      if (p) (void)hipFree(p);
+    for (void *p : ps) batchFree(p, s);
     b->d_fmtLen = b->d_fmtOff = nullptr;
     b->d_fmtIdx = nullptr;
     b->d_fmtTmp = nullptr;
-    b->d_fmtLen = devAlloc<uint64_t>((size_t)n + 1);
-    b->d_fmtOff = devAlloc<uint64_t>((size_t)n + 1);
-    b->d_fmtIdx = devAlloc<uint32_t>((size_t)n + 1);
+    b->d_fmtLen = bAlloc<uint64_t>((size_t)n + 1);
+    b->d_fmtOff = bAlloc<uint64_t>((size_t)n + 1);
+    b->d_fmtIdx = bAlloc<uint32_t>((size_t)n + 1);
     b->fmtTmpBytes = samScanTempBytes(n);
-    b->d_fmtTmp = devAlloc<uint8_t>(b->fmtTmpBytes);
+    b->d_fmtTmp = bAlloc<uint8_t>(b->fmtTmpBytes);
     b->fmtCap = (size_t)n + 1;
   }
-  if (!b->d_fmtErr) b->d_fmtErr = devAlloc<uint32_t>(1);
+  if (!b->d_fmtErr) b->d_fmtErr = bAlloc<uint32_t>(1);
   const uint32_t *dIdx = nullptr;
   if (hostIdx) {
     HIPCHK(hipMemcpyAsync(b->d_fmtIdx, hostIdx, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
@@ -1354,7 +1462,7 @@ static uint64_t formatOnDevice(gwa_batch *b, const uint32_t *hostIdx, uint32_t f
                                          : stt == ST_ERROR ? "reference would abort (exception) at read "
                                                            : "reference would abort (exception in AlignmentRecord.convert) at read ") + nm);
   }
-  growDev(&b->d_fmtText, &b->fmtTextCap, (size_t)total + 1);
+  growDev(&b->d_fmtText, &b->fmtTextCap, (size_t)total + 1, s);
   launchSamFormat(t, b->d_oh, b->d_hits, b->d_cig, dIdx, first, n, b->d_fmtLen, b->d_fmtOff, b->d_fmtTmp, &tmpBytes,
                   b->d_fmtErr, b->d_fmtText, 2, s, ps, total);
   HIPCHK(hipEventRecord(ev.e[1], s));
@@ -1518,8 +1626,8 @@ int gwa_batch_create_pairs(gwa_index_t *ix, const gwa_config_t *cfg, const gwa_r
     (*out)->pairs = n;
     (*out)->minIns = min_insert;
     (*out)->maxIns = max_insert;
-    (*out)->d_rescue = devAlloc<RescueOut>(n);
-    (*out)->d_heavy = devAlloc<uint32_t>((size_t)n + 2);  // list, its count, rescues skipped (window)
+    (*out)->d_rescue = bAlloc<RescueOut>(n);
+    (*out)->d_heavy = bAlloc<uint32_t>((size_t)n + 2);  // list, its count, rescues skipped (window)
     return 0;
   } catch (std::exception &e) {
     return fail(e.what());
