@@ -57,17 +57,22 @@ inline FILE *gwaVerifyLog() {
     const uint64_t d_ = clock64() - (v);                                        \
     if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) prof[r] += d_;      \
   } while (0)
-// GWA_PC(w, l): count one wavefront execution in slot w and one lane execution in slot l
+// GWA_PC(w, l): count one wavefront execution in slot w and one lane execution in slot l (counters
+// in the lane's global profile slots, profG: a register array of them broke the gfx950 backend)
 #define GWA_PC(w, l)                                                            \
   do {                                                                          \
-    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) prof[w] += 1;       \
-    prof[l] += 1;                                                               \
+    if (profG) {                                                                \
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) profG[w] += 1;    \
+      profG[l] += 1;                                                            \
+    }                                                                           \
   } while (0)
 // GWA_PW(w, e, b): a store of b bytes at one site: bytes in slot w, one lane event in slot e
 #define GWA_PW(w, e, b)                                                         \
   do {                                                                          \
-    prof[w] += (uint64_t)(b);                                                   \
-    prof[e] += 1;                                                               \
+    if (profG) {                                                                \
+      profG[w] += (uint64_t)(b);                                                \
+      profG[e] += 1;                                                            \
+    }                                                                           \
   } while (0)
 #else
 #define GWA_PT(v)
@@ -406,7 +411,8 @@ struct BsfLane {
   uint32_t *trace = nullptr;
   int traceCap = 0, traceN = 0;
 #ifdef GWA_PROF
-  uint64_t prof[PR_N] = {};
+  uint64_t prof[PR_N] = {};  // cycle regions (GWA_PA)
+  uint64_t *profG = nullptr; // this lane's global profile slots (GWA_PC / GWA_PW counters)
 #endif
   GWA_HD void tr(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     if (!trace || traceN + 4 > traceCap) return;
@@ -2071,17 +2077,136 @@ struct BsfLane {
   //   searchStep : one loop iteration (:343-477); SS_CONTINUE, SS_REPORT (run searchReport next)
   //                or SS_DONE
   //   searchReport: reportAlignment of the pending chain; false = the search ended (error/overflow)
-  enum { SS_CONTINUE = 0, SS_REPORT = 1, SS_DONE = 2 };
+  enum { SS_CONTINUE = 0, SS_REPORT = 1, SS_DONE = 2, SS_SUSPEND = 3 };
   int pendingBase = -1, upperSearches = 0;
-  GWA_HD void searchPhase(const ScanRes &sr) {
-    if (!searchStart(sr)) return;
-    for (;;) {
-      const int st = searchStep();
-      if (st == SS_DONE) return;
-      if (st == SS_REPORT && !searchReport()) return;
-    }
-  }
   GWA_HD bool searchReport() { return reportAlignment(pendingBase); }
+
+  // ---- suspend / resume across capacity tiers ----
+  // A read about to outgrow one of its lane's capacities is suspended between micro-steps -- its lane
+  // fields and the used part of its slice (arena, queue, hits, report list, CIGAR ops) copied to a
+  // record -- and resumed on the next, larger tier from that record instead of rerunning its search
+  // from the seeds.  Exactness: a micro-step is started only when it cannot overflow the arena or the
+  // queue (at most 9 states and 5 queue entries per step: two control rounds of split + clip children,
+  // then one child), and a report that overflows the hits, the CIGAR area or the first tier's DP slice
+  // is rolled back to its start (verify only appends) and suspended before it; a report also needs a
+  // free report-list entry (AlignmentResultHolder.add keeps at most listSize + 1).  Everything else a
+  // step or report touches is as it would be without the suspension.
+  enum { LP_RUN = 0, LP_WAIT = 1, LP_FINISH = 2, LP_SUSPEND = 3 };
+  int susPhase = LP_RUN;  // the phase a suspended read resumes in (LP_RUN or LP_WAIT: a report pending)
+  // room for one control round (controlPass) and the FM step it may end in, by where the round starts:
+  // a run-ahead (xMode 3) ends with at most one new state and one queue entry; a poll (0) is followed
+  // by a child (+1 state, +1 entry, the polled one gone) or the split and clip children (+4 states, +2
+  // entries); the choice of a child (1) by a child or the split children; the split stage (2) by
+  // those.  0 when there is room, else the OV_* capacity that may run out.
+  GWA_HD int passRoom() const {
+    const int a = xMode == 3 ? 1 : 4;
+    const int q = xMode == 3 ? 1 : xMode == 0 ? 1 : 2;
+    return nStates + a > caps.arena ? OV_ARENA : heapSize + q > caps.heap ? OV_HEAP : 0;
+  }
+  GWA_HD int laneStep() {
+    const int st = searchStep();
+    if (st == SS_SUSPEND) {
+      susPhase = LP_RUN;
+      return LP_SUSPEND;
+    }
+    return st == SS_REPORT ? LP_WAIT : st == SS_DONE ? LP_FINISH : LP_RUN;
+  }
+  GWA_HD int laneReport() {
+    if (listSize >= caps.list) {
+      ovfWhat |= OV_LIST;
+      susPhase = LP_WAIT;
+      return LP_SUSPEND;
+    }
+    const int h0 = nHits, c0 = nCigar, sw0 = numSW, vb0 = verifyBytes, sa0 = saReads, st0 = status;
+    if (searchReport()) return LP_RUN;
+    if (status == ST_OVERFLOW && (ovfWhat & ~(OV_HITS | OV_CIGAR | OV_SLICE)) == 0) {
+      nHits = h0;  // (verify appended hits and CIGAR ops only; nothing else changed yet)
+      nCigar = c0;
+      numSW = sw0;
+      verifyBytes = vb0;
+      saReads = sa0;
+      status = st0;
+      susPhase = LP_WAIT;
+      return LP_SUSPEND;
+    }
+    return LP_FINISH;
+  }
+  // record layout: header (lane fields, the cached state), then arena | queue | hits | list | CIGAR
+  static constexpr uint32_t kResumeMagic = 0x52534D31u;
+  static constexpr int kResumeInts = 48;
+  GWA_HD static size_t resumeHdrBytes() { return ((size_t)kResumeInts * 4 + 8 + sizeof(DState<R>) + 63) & ~(size_t)63; }
+  GWA_HD static size_t resumeBytes(const Caps &c) {
+    return resumeHdrBytes() + sizeof(DState<R>) * (size_t)c.arena + 8 * (size_t)c.heap + sizeof(DHit) * (size_t)c.hits +
+           4 * (size_t)c.list + 2 * (size_t)c.cigar + 64;
+  }
+  // no record for read r at rec (restart on the next tier)
+  GWA_HD static void resumeInvalidate(uint8_t *rec) { ((uint32_t *)rec)[0] = 0; }
+  GWA_HD void suspendTo(uint8_t *rec, uint32_t r) {
+    int32_t v[kResumeInts] = {};
+    int q = 1;  // (v[0]: the magic word, written last)
+    v[q++] = (int32_t)r;
+    v[q++] = minMismatches; v[q++] = maxMatchLength; v[q++] = bestScore; v[q++] = numFMIndexSearches;
+    v[q++] = nStates; v[q++] = heapSize; v[q++] = nHits; v[q++] = listSize; v[q++] = nCigar; v[q++] = listOk;
+    v[q++] = pendingBase; v[q++] = upperSearches; v[q++] = xMode; v[q++] = xT; v[q++] = xBase; v[q++] = xC;
+    v[q++] = xNm; v[q++] = xNextBase; v[q++] = xFirst; v[q++] = raIt; v[q++] = raMoved; v[q++] = raNs;
+    v[q++] = cacheIdx; v[q++] = cacheDirty; v[q++] = susPhase;
+    v[q++] = quickSteps; v[q++] = blocks; v[q++] = saReads; v[q++] = maxHeap; v[q++] = kmerLookups;
+    v[q++] = shortSteps; v[q++] = textSteps; v[q++] = textRuns; v[q++] = numSW; v[q++] = verifyBytes;
+    int32_t *h = (int32_t *)rec;
+    for (int i = 1; i < kResumeInts; ++i) h[i] = v[i];
+    *(uint64_t *)(rec + kResumeInts * 4) = raBound;
+    *(DState<R> *)(rec + kResumeInts * 4 + 8) = cache;
+    uint8_t *o = rec + resumeHdrBytes();
+    copyOut(o, (const uint8_t *)L.arena(), sizeof(DState<R>) * (size_t)nStates);
+    o += (sizeof(DState<R>) * (size_t)nStates + 15) & ~(size_t)15;
+    uint64_t *hq = (uint64_t *)o;
+    for (int i = 0; i < heapSize; ++i) hq[i] = hslot(i);
+    o += ((size_t)heapSize * 8 + 15) & ~(size_t)15;
+    copyOut(o, (const uint8_t *)L.hits(), sizeof(DHit) * (size_t)nHits);
+    o += (sizeof(DHit) * (size_t)nHits + 15) & ~(size_t)15;
+    int32_t *lo = (int32_t *)o;
+    for (int i = 0; i < listSize; ++i) lo[i] = L.list()[i];
+    o += ((size_t)listSize * 4 + 15) & ~(size_t)15;
+    uint16_t *co = (uint16_t *)o;
+    for (int i = 0; i < nCigar; ++i) co[i] = L.cigar()[i];
+    h[0] = (int32_t)kResumeMagic;  // (written last: the record is complete)
+  }
+  // true when rec holds read r's suspended search; then the lane continues it (phase in *phase)
+  GWA_HD bool resumeFrom(const uint8_t *rec, uint32_t r, int *phase) {
+    const int32_t *h = (const int32_t *)rec;
+    if ((uint32_t)h[0] != kResumeMagic || (uint32_t)h[1] != r) return false;
+    int q = 2;
+    minMismatches = h[q++]; maxMatchLength = h[q++]; bestScore = h[q++]; numFMIndexSearches = h[q++];
+    nStates = h[q++]; heapSize = h[q++]; nHits = h[q++]; listSize = h[q++]; nCigar = h[q++]; listOk = h[q++];
+    pendingBase = h[q++]; upperSearches = h[q++]; xMode = h[q++]; xT = h[q++]; xBase = h[q++]; xC = h[q++];
+    xNm = h[q++]; xNextBase = h[q++]; xFirst = h[q++]; raIt = h[q++]; raMoved = h[q++]; raNs = h[q++];
+    cacheIdx = h[q++]; cacheDirty = h[q++]; *phase = h[q++];
+    quickSteps = h[q++]; blocks = h[q++]; saReads = h[q++]; maxHeap = h[q++]; kmerLookups = h[q++];
+    shortSteps = h[q++]; textSteps = h[q++]; textRuns = h[q++]; numSW = h[q++]; verifyBytes = h[q++];
+    raBound = *(const uint64_t *)(rec + kResumeInts * 4);
+    cache = *(const DState<R> *)(rec + kResumeInts * 4 + 8);
+    const uint8_t *o = rec + resumeHdrBytes();
+    copyOut((uint8_t *)L.arena(), o, sizeof(DState<R>) * (size_t)nStates);
+    o += (sizeof(DState<R>) * (size_t)nStates + 15) & ~(size_t)15;
+    const uint64_t *hq = (const uint64_t *)o;
+    for (int i = 0; i < heapSize; ++i) hslot(i) = hq[i];
+    o += ((size_t)heapSize * 8 + 15) & ~(size_t)15;
+    copyOut((uint8_t *)L.hits(), o, sizeof(DHit) * (size_t)nHits);
+    o += (sizeof(DHit) * (size_t)nHits + 15) & ~(size_t)15;
+    const int32_t *lo = (const int32_t *)o;
+    for (int i = 0; i < listSize; ++i) L.list()[i] = lo[i];
+    o += ((size_t)listSize * 4 + 15) & ~(size_t)15;
+    const uint16_t *co = (const uint16_t *)o;
+    for (int i = 0; i < nCigar; ++i) L.cigar()[i] = co[i];
+    buildMasks();  // the read words / QueryMask rows in LDS (searchStart builds them on a fresh start)
+    status = ST_UNMAPPED;
+    ovfWhat = 0;
+    return true;
+  }
+  // n bytes (a multiple of 8, both ends 8-B aligned) 8 B at a time
+  GWA_HD static void copyOut(uint8_t *dst, const uint8_t *src, size_t n) {
+    for (size_t i = 0; i < n / 8; ++i) ((uint64_t *)dst)[i] = ((const uint64_t *)src)[i];
+  }
   GWA_HD bool searchStart(const ScanRes &sr) {
     GWA_PT(tsd);
     buildMasks();
@@ -2235,10 +2360,16 @@ struct BsfLane {
     DState<R> P;  // the parent of this call's FM step (a register copy)
     int ch = -1, kind = 0;  // the FM step's base; kind 1: a child of xC, 2: a run-ahead step
     GWA_PC(PR_NSW, PR_NSL);
-    // kPasses = 2 rounds of control work, written out (no loop: early exits from divergent loops
-    // have been mis-lowered on gfx950)
+    // two rounds of control work, written out (no loop: early exits from divergent loops have been
+    // mis-lowered on gfx950); a round starts only when it cannot overflow the
+    // arena or the queue (passRoom), else the read is suspended here (before the first) or the call
+    // ends (before the second)
+    if (const int ov = passRoom()) {
+      ovfWhat |= ov;
+      return SS_SUSPEND;
+    }
     int cp = controlPass(P, ch, kind);
-    if (cp == CP_AGAIN) cp = controlPass(P, ch, kind);
+    if (cp == CP_AGAIN && passRoom() == 0) cp = controlPass(P, ch, kind);
     if (cp == CP_DONE) return SS_DONE;
     if (cp == CP_REPORT) return SS_REPORT;
     if (cp != CP_STEP) return SS_CONTINUE;

@@ -1069,6 +1069,22 @@ int gwa_batch_run(gwa_batch_t *b) {
     if (const char *e = getenv("GWA_MAX_STATES_LOG2"))  // diagnostics (tools/diag_sf.py): a lower state limit
       arenaMaxLog = std::max(16, std::min(24, atoi(e)));
     const bool hybrid = !sf && b->R >= 8;
+    // resume records (-m bsf): a tier writes those of the reads it suspends into resOut (entry i of its
+    // overflow list), the next tier reads them from resIn (bsf_search_kernel, BsfLane::suspendTo)
+    struct ResBuf {
+      uint8_t *p = nullptr;
+      size_t bytes = 0;
+      uint64_t stride = 0;
+      uint32_t cap = 0;
+    } resIn, resOut;
+    struct ResFree {  // (the batch's stream is drained before the buffers go back)
+      ResBuf *a, *b;
+      hipStream_t s;
+      ~ResFree() {
+        batchFree(a->p, s);
+        batchFree(b->p, nullptr);
+      }
+    } resFree{&resIn, &resOut, s};
     // the capacities of tier tb (the last one grown by the g* shifts)
     auto capsFor = [&](int tb) {
       const Tier &T = sf ? kSfTiers[tb] : kTiers[tb];
@@ -1183,6 +1199,26 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipMemsetAsync(ovfCount, 0, 4, s));
       HIPCHK(hipMemsetAsync(b->d_count + 8 + tb, 0, 4, s));
       HIPCHK(hipMemsetAsync(ovfBits, 0, 4, s));
+      ResumeBufs rb{};
+      if (!sf) {
+        const uint64_t rstride = resumeBytesFor(b->R, caps);
+        const uint64_t cap = std::min<uint64_t>(n, std::min<uint64_t>(8ull << 30, budget / 4) / rstride);
+        if (resOut.bytes < cap * rstride) {
+          batchFree(resOut.p, s);
+          resOut.p = nullptr;
+          resOut.bytes = 0;
+          resOut.p = bAlloc<uint8_t>(cap * rstride);
+          resOut.bytes = cap * rstride;
+        }
+        resOut.stride = rstride;
+        resOut.cap = (uint32_t)cap;
+        rb.out = cap ? resOut.p : nullptr;
+        rb.outStride = rstride;
+        rb.outCap = (uint32_t)cap;
+        rb.in = resIn.cap ? resIn.p : nullptr;
+        rb.inStride = resIn.stride;
+        rb.inCap = resIn.cap;
+      }
       HIPCHK(hipEventRecord(e1, s));
       const OutSlots os = outSlots(b);
 #ifdef GWA_PROF
@@ -1192,7 +1228,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
       launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                    scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount,
-                   ovfBits, s, (uint32_t *)d_prof, -1);
+                   ovfBits, rb, s, (uint32_t *)d_prof, -1);
       {
         std::vector<uint64_t> pv((size_t)lanes * PR_N);
         HIPCHK(hipMemcpyAsync(pv.data(), d_prof, pv.size() * 8, hipMemcpyDeviceToHost, s));
@@ -1222,7 +1258,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       else
         launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                      scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1],
-                     ovfCount, ovfBits, s);
+                     ovfCount, ovfBits, rb, s);
 #endif
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(e2, s));
@@ -1240,6 +1276,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       n = ctr[1 + tb];
       const uint32_t bits = ctr[15];
       cur ^= 1;
+      if (!sf) std::swap(resIn, resOut);  // this tier's records are the next one's input
       if (n > 0) {  // the reads rerun on the next tier (instrumentation, gwa_batch_read_counters)
         std::vector<uint32_t> ids(n);
         HIPCHK(hipMemcpyAsync(ids.data(), b->d_list[cur], n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));

@@ -309,12 +309,12 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
                   const StairTables &st, const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n,
                   uint8_t *scratch, uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,
                   const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
-                  hipStream_t s, uint32_t *trace, int traceRead) {
+                  const ResumeBufs &res, hipStream_t s, uint32_t *trace, int traceRead) {
   if (n == 0) return;
 #define GWA_L(Q, RR)                                                                                                   \
   if (QW == Q && R == RR) {                                                                                            \
     launchSearchQR<Q, RR>(ldsHeap, lanes, ix, cfg, st, reads, sres, list, n, scratch, laneStride, caps, oh, os, chrRank, \
-                          work, ovfList, ovfCount, ovfBits, s, trace, traceRead);                                      \
+                          work, ovfList, ovfCount, ovfBits, res, s, trace, traceRead);                                 \
     return;                                                                                                            \
   }
 #define GWA_LQ(Q) GWA_L(Q, 4) GWA_L(Q, 8) GWA_L(Q, 16) GWA_L(Q, 32)
@@ -350,5 +350,13 @@ size_t laneBytesFor(int R, const Caps &c) {
   }
 }
 size_t ilvBytesFor(const Caps &c) { return ilvBytes(c); }
+size_t resumeBytesFor(int R, const Caps &c) {
+  switch (R) {
+    case 4: return BsfLane<4>::resumeBytes(c);
+    case 8: return BsfLane<8>::resumeBytes(c);
+    case 16: return BsfLane<16>::resumeBytes(c);
+    default: return BsfLane<32>::resumeBytes(c);
+  }
+}
 
 }  // namespace gwa

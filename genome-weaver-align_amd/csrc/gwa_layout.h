@@ -205,6 +205,16 @@ struct RescueOut {
 constexpr int64_t kPairQuad = 64;
 constexpr int kPairSortCap = 4096;  // candidates of both mates one workgroup sorts in LDS
 
+// Resume records of the reads a search tier suspends (BsfLane::suspendTo / resumeFrom): record i
+// belongs to entry i of the tier's overflow list (= the next tier's read list); a tier reads `in`
+// (the previous tier's records) and writes `out` (null: none kept, the reads restart)
+struct ResumeBufs {
+  const uint8_t *in;
+  uint8_t *out;
+  uint64_t inStride, outStride;
+  uint32_t inCap, outCap;
+};
+
 // quick-scan outcome carried from fm_quickscan to bsf_search (FMQuickScan fields used at
 // S/BidirectionalSuffixFilter.java:324-346)
 struct ScanRes {

@@ -17,7 +17,8 @@ void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &i
                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                   uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,
                   const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
-                  hipStream_t s, uint32_t *trace = nullptr, int traceRead = -1);
+                  const ResumeBufs &res, hipStream_t s, uint32_t *trace = nullptr, int traceRead = -1);
+size_t resumeBytesFor(int R, const Caps &c);  // one resume record of a tier with capacities c
 void launchSfSearch(int R, int QW, bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                     const Caps &caps, OutHeader *oh, const OutSlots &os,

@@ -11,18 +11,19 @@
 namespace gwa {
 
 
-__device__ __forceinline__ void waveAppend(bool need, uint32_t value, uint32_t *list, uint32_t *count) {
+// appends value to list (one atomic per wavefront); returns the lane's position (needing lanes)
+__device__ __forceinline__ uint32_t waveAppend(bool need, uint32_t value, uint32_t *list, uint32_t *count) {
   const uint64_t mask = __ballot(need);
-  if (mask == 0) return;
+  if (mask == 0) return 0;
   const int lane = __lane_id();
   const int leader = __ffsll((long long)mask) - 1;
   uint32_t base = 0;
   if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
   base = __shfl(base, leader);
-  if (need) {
-    const uint64_t below = lane == 0 ? 0ULL : (mask & ((~0ULL) >> (64 - lane)));
-    list[base + __popcll(below)] = value;
-  }
+  const uint64_t below = lane == 0 ? 0ULL : (mask & ((~0ULL) >> (64 - lane)));
+  const uint32_t pos = base + (uint32_t)__popcll(below);
+  if (need) list[pos] = value;
+  return pos;
 }
 
 template <int QW>
@@ -63,7 +64,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
                                                          uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
                                                          const int32_t *chrRank,
                                                          uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount,
-                                                         uint32_t *ovfBits, uint32_t *trace, int traceRead) {
+                                                         uint32_t *ovfBits, ResumeBufs res, uint32_t *trace, int traceRead) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
   // scratch = [active lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]; a
@@ -103,6 +104,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   }
   typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8))> Lane;  // hybrid heap: k >= 4 with the LDS heap, sparse tiers
   Lane lane(ix, cfg, st, L, caps);
+#ifdef GWA_PROF
+  lane.profG = prof;
+#endif
   lane.chrRank = chrRank;
   if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
   __shared__ uint64_t qwLds[2 * QW * 256];  // the lanes' 2-bit read words (BsfLane::qword)
@@ -117,7 +121,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
   // the wavefront runs the parked reports (DP verification + traceback) together once they are at
   // least half of its live lanes, instead of once per lane on a divergent path.
-  enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED };
+  enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED, SUSPEND };
   int phase = IDLE;
   uint32_t r = 0;
   // deep tiers with few reads (caps.sparse > 1): only every caps.sparse-th lane takes reads, so the
@@ -142,7 +146,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
           lane.trace = nullptr;
           if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; lane.traceN = 0; }
           lane.initRead(reads.codes + o, m);
-          phase = lane.searchStart(sres[r]) ? RUN : FINISH;
+          // a read the previous tier suspended continues from its record (Lane::resumeFrom)
+          int rp = 0;
+          if (res.in && i < res.inCap && lane.resumeFrom(res.in + (size_t)i * res.inStride, r, &rp))
+            phase = rp == Lane::LP_WAIT ? WAIT : RUN;
+          else
+            phase = lane.searchStart(sres[r]) ? RUN : FINISH;
         } else {
           phase = EXHAUSTED;
         }
@@ -158,13 +167,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 #ifdef GWA_PROF
       const uint64_t trp = clock64();
 #endif
-      if (phase == WAIT) phase = lane.searchReport() ? RUN : FINISH;
+      if (phase == WAIT) {
+        const int lp = lane.laneReport();
+        phase = lp == Lane::LP_RUN ? RUN : lp == Lane::LP_SUSPEND ? SUSPEND : FINISH;
+      }
 #ifdef GWA_PROF
       if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) lane.prof[PR_REPORT] += clock64() - trp;
 #endif
     } else if (phase == RUN) {
-      const int sst = lane.searchStep();
-      phase = sst == Lane::SS_REPORT ? WAIT : sst == Lane::SS_DONE ? FINISH : RUN;
+      const int lp = lane.laneStep();
+      phase = lp == Lane::LP_WAIT ? WAIT : lp == Lane::LP_FINISH ? FINISH : lp == Lane::LP_SUSPEND ? SUSPEND : RUN;
     }
     bool ovf = false;
     if (phase == FINISH) {
@@ -172,9 +184,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
       if (lane.trace) trace[0] = (uint32_t)lane.traceN;
       ovf = oh[r].status == ST_OVERFLOW;
       if (ovf) atomicOr(ovfBits, (uint32_t)oh[r].ovfWhat);
-      phase = IDLE;
+    } else if (phase == SUSPEND) {  // the next tier resumes it from its record
+      lane.status = ST_OVERFLOW;
+      lane.writeSearchOutput(oh + r, os, r);
+      atomicOr(ovfBits, (uint32_t)lane.ovfWhat);
+      ovf = true;
     }
-    waveAppend(ovf, r, ovfList, ovfCount);
+    const uint32_t pos = waveAppend(ovf, r, ovfList, ovfCount);
+    if (ovf && res.out && pos < res.outCap) {
+      uint8_t *rec = res.out + (size_t)pos * res.outStride;
+      if (phase == SUSPEND) lane.suspendTo(rec, r);
+      else Lane::resumeInvalidate(rec);
+    }
+    if (phase == FINISH || phase == SUSPEND) phase = IDLE;
   }
 #ifdef GWA_PROF
   for (int q = 0; q < PR_N - 1; ++q) prof[q] += lane.prof[q];
@@ -266,12 +288,12 @@ template <int QW, int R>
 void launchSearchQR(int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                     const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                     uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank,
-                    uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s,
-                    uint32_t *trace, int traceRead) {
+                    uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, const ResumeBufs &res,
+                    hipStream_t s, uint32_t *trace, int traceRead) {
   dim3 grid((lanes + 255) / 256);
 #define GWA_CASE(LL)                                                                                                   \
   hipLaunchKernelGGL((bsf_search_kernel<R, QW, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n, scratch,  \
-                     laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, trace, traceRead)
+                     laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, res, trace, traceRead)
   if (ldsHeap == 2) GWA_CASE(2);
   else if (ldsHeap) GWA_CASE(1);
   else GWA_CASE(0);
@@ -300,7 +322,8 @@ void launchSfSearchQR(bool wrap, uint32_t lanes, const IndexView &ix, const Sear
   KW void launchSearchQR<QW_, R_>(int, uint32_t, const IndexView &, const SearchConfig &, const StairTables &,     \
                                   const ReadsView &, const ScanRes *, const uint32_t *, uint32_t, uint8_t *, uint64_t, \
                                   const Caps &, OutHeader *, const OutSlots &, const int32_t *, uint32_t *,        \
-                                  uint32_t *, uint32_t *, uint32_t *, hipStream_t, uint32_t *, int);               \
+                                  uint32_t *, uint32_t *, uint32_t *, const ResumeBufs &, hipStream_t, uint32_t *, \
+                                  int);                                                                            \
   KW void launchSfSearchQR<QW_, R_>(bool, uint32_t, const IndexView &, const SearchConfig &, const StairTables &,  \
                                     const ReadsView &, const uint32_t *, uint32_t, uint8_t *, uint64_t,           \
                                     const Caps &, OutHeader *, const OutSlots &, const int32_t *, uint32_t *,      \

@@ -152,7 +152,8 @@ def lib():
         L.gwa_reads_shard_range.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, P(U64), P(U64)]
         L.gwa_pipeline_stats.argtypes = [V, P(PipelineStats)]
         L.gwa_pipeline_close.argtypes = [V]
-        L.gwa_snappy_decompress.argtypes = [ctypes.c_char_p, U64, P(V), P(U64)]
+        if hasattr(L, "gwa_snappy_decompress"):  # (older libraries in A/B runs lack it)
+            L.gwa_snappy_decompress.argtypes = [ctypes.c_char_p, U64, P(V), P(U64)]
         _lib = L
     return _lib
 

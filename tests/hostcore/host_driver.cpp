@@ -23,6 +23,8 @@ struct HC {
   std::vector<uint64_t> kmer[2];
 };
 
+static uint64_t g_suspends = 0;  // reads suspended (and resumed on the next tier), all calls
+
 // the GPU's capacity tiers (gwa_api.cpp kTiers) replayed on the CPU
 template <int R, int QW>
 static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTables &st, int maxM, int kmax, uint32_t n,
@@ -63,6 +65,9 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
     OutHeader hd{};
     std::vector<uint32_t> tv(65537, 0);
     bool traced = false;
+    std::vector<uint8_t> rec;  // the read's resume record from the tier that suspended it
+    bool haveRec = false, quickDone = false;
+    ScanRes sr{};
     // tiers 0-3, then the last tier with every capacity doubled per rerun (gwa_batch_run grows the
     // exceeded ones; doubling all of them gives the same results, capacities only decide overflow)
     for (int t = 0; t < 14; ++t) {
@@ -101,15 +106,42 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
       }
       LaneMem<R> L = laneMem<R>(scratch.data(), bc);
       BsfLane<R, QW> lane(x->v, cfg, st, L, bc);
+      typedef BsfLane<R, QW> Lane;
       lane.chrRank = rk.data();
       const char *tre = getenv("GWA_TRACE_READ");
       const char *qtre = getenv("GWA_QTRACE_READ");
       if ((tre && atoi(tre) == (int)i) || (qtre && atoi(qtre) == (int)i)) { lane.trace = tv.data() + 1; lane.traceCap = 65536; traced = true; }
       lane.initRead(codes.data(), (int)mlen);
-      ScanRes sr{};
       used[0] = used[1] = used[2] = 0;
-      if (lane.quickPhase(&sr, &hd, os, 0)) {
-        lane.searchPhase(sr);
+      // the kernel's lane loop (search_kernels.h bsf_search_kernel): steps and reports until the read
+      // finishes or is suspended; a suspended read resumes on the next tier from its record, as there
+      // (HC_NO_RESUME=1: every overflow restarts from the seeds, the pre-resume behaviour)
+      int phase = Lane::LP_FINISH;
+      int rp = 0;
+      if (haveRec && lane.resumeFrom(rec.data(), i, &rp)) {
+        phase = rp;
+      } else if (t == 0 || !quickDone) {
+        quickDone = true;
+        phase = lane.quickPhase(&sr, &hd, os, 0) ? (lane.searchStart(sr) ? Lane::LP_RUN : Lane::LP_FINISH) : -1;
+      } else {
+        phase = lane.searchStart(sr) ? Lane::LP_RUN : Lane::LP_FINISH;
+      }
+      haveRec = false;
+      if (phase == -1) {  // the quick scan finished the read
+        if (traced) tv[0] = (uint32_t)lane.traceN;
+        break;
+      }
+      while (phase == Lane::LP_RUN || phase == Lane::LP_WAIT) phase = phase == Lane::LP_RUN ? lane.laneStep() : lane.laneReport();
+      if (phase == Lane::LP_SUSPEND) {
+        lane.status = ST_OVERFLOW;
+        lane.writeSearchOutput(&hd, os, 0);
+        if (!getenv("HC_NO_RESUME")) {
+          rec.assign(Lane::resumeBytes(bc), 0);
+          lane.suspendTo(rec.data(), i);
+          haveRec = true;
+        }
+        ++g_suspends;
+      } else {
         lane.writeSearchOutput(&hd, os, 0);
       }
       if (traced) tv[0] = (uint32_t)lane.traceN;
@@ -185,6 +217,8 @@ void *hc_index_fasta(const char *text, uint64_t len) {
 }
 
 void hc_index_free(void *p) { delete (HC *)p; }
+
+uint64_t hc_suspends(void) { return g_suspends; }
 
 int hc_sa(void *p, int strand, uint32_t *out) {
   auto *x = (HC *)p;

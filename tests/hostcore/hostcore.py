@@ -23,6 +23,7 @@ def lib():
         L.hc_index_fasta.restype = ctypes.c_void_p
         L.hc_index_fasta.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
         L.hc_index_free.argtypes = [ctypes.c_void_p]
+        L.hc_suspends.restype = ctypes.c_uint64
         L.hc_sa.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.hc_align.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                ctypes.c_void_p,
@@ -69,3 +70,8 @@ class HostCore:
             raise RuntimeError("hostcore align failed rc=%d" % rc)
         s = ctypes.string_at(out, ln.value).decode()
         return (s, st.reshape(n, 4)) if stats else s
+
+
+def suspends():
+    """reads the host replay of the tiers has suspended and resumed so far (all calls)"""
+    return lib().hc_suspends()

@@ -306,3 +306,32 @@ def test_sf_wrap_instance_rule():
     assert wraps and max(m for m, _ in wraps) <= 31
     assert any(L.hc_sf_chunks_wrap(m, kk) for m in range(129, 257) for kk in range(1, 33))
     assert any(L.hc_sf_chunks_wrap(m, kk) for m in range(257, 513) for kk in range(1, 33))
+
+
+# ---- suspend / resume across capacity tiers (BsfLane::suspendTo / resumeFrom) ----
+
+@pytest.mark.parametrize("arena", [24, 48])
+def test_suspend_resume_across_tiers(random_genome, repetitive_genome, monkeypatch, arena):
+    """A read about to outgrow its tier is suspended between micro-steps (or before a report, which an
+    overflow rolls back) and resumed on the next tier from its record instead of restarting from the
+    seeds.  With a tiny first tier most searches suspend; the SAM and every read's FM-search and DP
+    counts equal the oracle's, and equal a replay where every overflow restarts."""
+    monkeypatch.setenv("HC_T0_ARENA", str(arena))
+    cases = []
+    codes, names, lengths = random_genome
+    seqs, rn = synth.reads(codes, lengths, 150, 150, config_id=4, indels=True, max_edits=5)
+    strs = synth.to_strings(seqs)
+    cases.append((random_genome, [(rn[i], strs[i], None) for i in range(len(strs))], 5.0))
+    cases.append((repetitive_genome, _mk(repetitive_genome[0], 150, 100, 2, True, seed=9), 2.0))
+    for (codes, names, lengths), reads, k in cases:
+        oi = O.Index.from_arrays(codes, names, lengths)
+        hc = hostcore.HostCore(codes, names, lengths)
+        s0 = hostcore.suspends()
+        got, st = hc.align(reads, k=k, stats=True)
+        assert hostcore.suspends() - s0 >= 10
+        exp, est = oi.align(reads, O.OrcConfig.default(k=k), with_stats=True)
+        assert got == exp
+        assert np.array_equal(st[:, 0], np.array([x.fm_searches for x in est]))
+        monkeypatch.setenv("HC_NO_RESUME", "1")
+        assert hc.align(reads, k=k) == got
+        monkeypatch.delenv("HC_NO_RESUME")
