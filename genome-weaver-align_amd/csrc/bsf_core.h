@@ -1411,8 +1411,6 @@ struct BsfLane {
       pT[r] = on ? dpPeq(strand, qs, qe, r, 3) : 0ULL;
     }
     const size_t is = (size_t)L.is;
-    VpVn *hist = (VpVn *)L.chunk + L.lane;  // [col 0..N][block]: the value the reference's history holds
-    const uint64_t *h8 = (const uint64_t *)L.chunk + L.lane;  // [col 0..N]: first-tier slices
     uint64_t vp[DB], vn[DB];
     int D[DB] = {}, sb[DB];
 #pragma unroll
@@ -1431,26 +1429,70 @@ struct BsfLane {
     RefWindow<QW + 2, QW / 2 + 1> rw;
     if (N > 32 * (QW + 2)) { ovf(OV_DP); return -1; }
     rw.load(ix.text2, ix.textN, ix.N, refStart);
+    // One column of the pass (:420-473) for reference code ch: the blocks are computed with selects,
+    // not divergent branches; blocks past bCeil give values nobody reads, except block bCeil, whose
+    // input is set to ~0 / 0 first -- if it is activated at this column (:427-428) its carry-in is
+    // that of the active blocks above it, as there.  Blocks from 2 on are skipped (uniform branch) when
+    // no lane of the wavefront needs them.  Afterwards the blocks not computed here are zeroed (what
+    // the reference's zero-initialised history holds for them).  Returns the block activated with
+    // this column as its input, or -1.
+    auto column = [&](int ch, uint64_t (&cp)[DB], uint64_t (&cn)[DB], int (&cD)[DB], int &cb) -> int {
+      int carry = 0, cIn = 0, nsC = 0;
+      uint64_t nextPeq = 0;
+#pragma unroll
+      for (int r = 0; r < DB; ++r) {
+        int ns = 0;
+        if (r < 2 || anyLane(r <= cb && r < bMax)) {
+          if (r == cb) { cp[r] = ~0ULL; cn[r] = 0ULL; }
+          const uint64_t xr = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
+          const int hin = carry;
+          ns = dpBlock(xr, hin, cp[r], cn[r]);
+          if (r < cb) cD[r] += ns;
+          if (r == cb) { cIn = hin; nsC = ns; nextPeq = xr; }  // hin = ns of block cb - 1
+        }
+        carry = ns;
+      }
+      const int bOld = cb;
+      const int dPrev = pick(cD, cb - 1);
+      const int act = cb < bMax && dPrev - cIn <= pick(sb, cb - 1) && (((nextPeq & 1ULL) != 0ULL) || cIn < 0);
+      const int actBlock = act ? cb : -1;
+#pragma unroll
+      for (int r = 0; r < DB; ++r) {
+        if (r == actBlock) cD[r] = dPrev - cIn + nsC;
+        if (!(r < bOld || r == actBlock)) { cp[r] = 0ULL; cn[r] = 0ULL; }  // not computed at this column
+      }
+      if (act) {
+        cb++;
+      } else {
+#pragma unroll
+        for (int q = 0; q < DB - 1; ++q)
+          if (cb > 1 && pick(cD, cb - 1) > pick(sb, cb - 1) + w) --cb;
+      }
+      return actBlock;
+    };
+    // No per-column history: every kCk columns the pass keeps its state (vp / vn of every block, the
+    // block scores, the active block count) as a checkpoint, element e of this lane's interleaved area
+    // at chunk[e * is + lane]; the traceback recomputes the column an edit needs from the checkpoint at
+    // or before it (below).  ~6 words per 16 columns instead of one word per column (first tier) or
+    // 16 B per block per column (deeper tiers), and no traceback ever leaves the kept rows.
+    constexpr int kCk = 16, kCw = 2 * DB + (DB + 2) / 2;  // checkpoint words
+    uint64_t *ckBase = (uint64_t *)L.chunk + L.lane;
+    if ((size_t)((N + kCk - 1) / kCk + 1) * kCw > (size_t)caps.dpWords) { ovf(OV_DP); return -1; }
+    auto ckStore = [&](int t) {
+      uint64_t *e = ckBase + (size_t)t * kCw * is;
+#pragma unroll
+      for (int r = 0; r < DB; ++r)
+        if (r < bMax) { e[(2 * r) * is] = vp[r]; e[(2 * r + 1) * is] = vn[r]; }
+#pragma unroll
+      for (int r = 0; r <= DB; r += 2) {
+        const uint32_t a = (uint32_t)(r < DB ? D[r] : bCeil);
+        const uint32_t b2 = (uint32_t)(r + 1 < DB ? D[r + 1] : r + 1 == DB ? bCeil : 0);
+        e[(2 * DB + r / 2) * is] = (uint64_t)a | ((uint64_t)b2 << 32);
+      }
+      GWA_PW(PR_WD, PR_ED, 8 * (2 * bMax + (DB + 2) / 2));
+      GWA_PC(PR_EDW, PR_N - 2);
+    };
     GWA_PT(tdf);
-    // Column c of the history holds, per block, what the reference's zero-initialised arrays hold
-    // after the whole pass: ~0 / 0 when the block was activated with input column c (the later
-    // write), else the value computed at column c - 1, else 0 / 0.  Iteration j stores column j + 1
-    // (blocks not computed at j are zeroed in their registers first: nothing reads those values,
-    // a block is re-initialised when it is activated) and, when it activates a block, rewrites
-    // that block's rows of column j to ~0 / 0.  The traceback then reads one word per edit and
-    // nothing else (no per-column flags).
-    // First tier (caps.dpSlice): only rows [lo, lo + 32) of column c are kept, lo = c - c0 - 17
-    // around the window's middle diagonal c0 = (N - mq) / 2 (= k, the read's offset x - refStart
-    // in the window, :507, away from the text ends), as one {vp 32 | vn 32} word -- 8 B per column
-    // instead of 16 B per block.  A traceback that leaves the slice overflows the read into the
-    // next tier, which keeps whole columns.  (dpSlice - 1 shifts the slice: tests only.)
-    // (column 0, the input column, is never read: the traceback reads columns col + 1 >= 1)
-    const bool slice = caps.dpSlice != 0;
-    const int c0 = ((N - mq) >> 1) + (slice ? caps.dpSlice - 1 : 0);
-    const size_t colStep = (size_t)bMax * is;
-    VpVn *hc = hist;                                // column j (full columns)
-    uint64_t *hc8 = (uint64_t *)L.chunk + L.lane;   // column j (slices)
-    uint64_t lastWord = 0;                          // the slice word of column j
     uint64_t run2 = 0, runN = 0;  // the window's codes from column j on (the loop index is uniform)
     for (int j = 0; j < N; ++j) {
       if ((j & 31) == 0) run2 = pick(rw.c2, j >> 5);
@@ -1458,64 +1500,8 @@ struct BsfLane {
       const int ch = (runN & 1ULL) ? 4 : (int)(run2 & 3ULL);
       run2 >>= 2;
       runN >>= 1;
-      // blocks are computed with selects, not divergent branches: blocks past bCeil give values
-      // nobody reads, except block bCeil, whose input is set to ~0 / 0 first -- if it is activated
-      // at this column (:427-428) its carry-in is that of the active blocks above it, as there.
-      // Blocks from 2 on are skipped (uniform branch) when no lane of the wavefront needs them.
-      int carry = 0, cIn = 0, nsC = 0;
-      uint64_t nextPeq = 0;
-#pragma unroll
-      for (int r = 0; r < DB; ++r) {
-        int ns = 0;
-        if (r < 2 || anyLane(r <= bCeil && r < bMax)) {
-          if (r == bCeil) { vp[r] = ~0ULL; vn[r] = 0ULL; }
-          const uint64_t xr = ch == 0 ? pA[r] : ch == 1 ? pC[r] : ch == 2 ? pG[r] : ch == 3 ? pT[r] : 0ULL;
-          const int hin = carry;
-          ns = dpBlock(xr, hin, vp[r], vn[r]);
-          if (r < bCeil) D[r] += ns;
-          if (r == bCeil) { cIn = hin; nsC = ns; nextPeq = xr; }  // hin = ns of block bCeil - 1
-        }
-        carry = ns;
-      }
-      const int bOld = bCeil;
-      const int dPrev = pick(D, bCeil - 1);
-      const int act = bCeil < bMax && dPrev - cIn <= pick(sb, bCeil - 1) && (((nextPeq & 1ULL) != 0ULL) || cIn < 0);
-      const int actBlock = act ? bCeil : -1;
-#pragma unroll
-      for (int r = 0; r < DB; ++r) {
-        if (r == actBlock) D[r] = dPrev - cIn + nsC;
-        if (!(r < bOld || r == actBlock)) { vp[r] = 0ULL; vn[r] = 0ULL; }  // not computed at j
-      }
-      if (act) {
-        bCeil++;
-      } else {
-#pragma unroll
-        for (int q = 0; q < DB - 1; ++q)
-          if (bCeil > 1 && pick(D, bCeil - 1) > pick(sb, bCeil - 1) + w) --bCeil;
-      }
-      if (slice) {
-        if (act) {  // rows of block actBlock in column j's slice: vp 1, vn 0
-          const int lo = j - c0 - 17, r0 = 64 * actBlock - lo, r1 = r0 + 64;
-          const int s0 = r0 < 0 ? 0 : r0 > 32 ? 32 : r0, s1 = r1 < 0 ? 0 : r1 > 32 ? 32 : r1;
-          const uint64_t msk = ((s1 >= 32 ? 0xFFFFFFFFULL : (1ULL << s1) - 1ULL) & ~((1ULL << s0) - 1ULL));
-          *hc8 = (lastWord | msk) & ~(msk << 32);
-          GWA_PW(PR_WD, PR_ED, 8);
-        }
-        const int lo1 = j - c0 - 16;
-        lastWord = (uint64_t)rows32(vp, lo1) | ((uint64_t)rows32(vn, lo1) << 32);
-        hc8[is] = lastWord;
-        GWA_PW(PR_WD, PR_ED, 8);
-        GWA_PC(PR_EDW, PR_N - 2);
-      } else {
-        if (act) { GWA_PW(PR_WD, PR_ED, 16); hc[(size_t)actBlock * is] = VpVn{~0ULL, 0ULL}; }
-        GWA_PW(PR_WD, PR_ED, 16 * bMax);
-        GWA_PC(PR_EDW, PR_N - 2);
-#pragma unroll
-        for (int r = 0; r < DB; ++r)
-          if (r < bMax) hc[colStep + r * is] = VpVn{vp[r], vn[r]};
-      }
-      hc += colStep;
-      hc8 += is;
+      if ((j & (kCk - 1)) == 0) ckStore(j / kCk);  // the state entering column j
+      column(ch, vp, vn, D, bCeil);
       if (bCeil == bMax) {
         const int dl = pick(D, bCeil - 1);
         if (!have) { have = 1; bestTail = j; bestDiff = dl; continue; }
@@ -1524,6 +1510,7 @@ struct BsfLane {
     }
     GWA_PA(PR_DPF, tdf);
     (void)bestDiff;
+    (void)caps.dpSlice;  // (the first tier's DP slice is gone: checkpoints serve every tier)
     if (!have) return 1;
     GWA_PT(tdt);
     // Traceback (:515-643).  A match decides the step from the codes alone (:547), so the history is
@@ -1592,18 +1579,34 @@ struct BsfLane {
         emit(0, runLen);
       }
       if (col >= 0 && row >= 0) {
+        // the history the reference holds for column c = col + 1 (:532-546), recomputed: the value
+        // column c - 1 computed, unless the block of this row was activated with input column c
+        // (then ~0 / 0), from the checkpoint at or before column c - 1
         int bp, bn;
-        if (slice) {
-          const int rr = row - (col + 1 - c0 - 17);
-          if (rr < 0 || rr >= 32) { ovf(OV_SLICE); return -1; }  // off the slice: next tier
-          const uint64_t h = h8[(size_t)(col + 1) * is];
-          bp = (int)(h >> rr) & 1;
-          bn = (int)(h >> (32 + rr)) & 1;
-        } else {
-          const int block = row >> 6, offset = row & 63;
-          const VpVn h = hist[((size_t)(col + 1) * bMax + block) * is];
-          bp = (int)(h.vp >> offset) & 1;
-          bn = (int)(h.vn >> offset) & 1;
+        {
+          const int c = col + 1, block = row >> 6, offset = row & 63;
+          const int t = (c - 1) / kCk;
+          uint64_t rp[DB], rn[DB];
+          int rD[DB], rb;
+          const uint64_t *e = ckBase + (size_t)t * kCw * is;
+#pragma unroll
+          for (int r = 0; r < DB; ++r) {
+            rp[r] = r < bMax ? e[(2 * r) * is] : 0ULL;
+            rn[r] = r < bMax ? e[(2 * r + 1) * is] : 0ULL;
+          }
+#pragma unroll
+          for (int r = 0; r <= DB; r += 2) {
+            const uint64_t x = e[(2 * DB + r / 2) * is];
+            if (r < DB) rD[r] = (int)(uint32_t)x;
+            else rb = (int)(uint32_t)x;
+            if (r + 1 < DB) rD[r + 1] = (int)(uint32_t)(x >> 32);
+            else if (r + 1 == DB) rb = (int)(uint32_t)(x >> 32);
+          }
+          for (int j = t * kCk; j < c; ++j) column(rw.code(j), rp, rn, rD, rb);
+          uint64_t hp = pick(rp, block), hn = pick(rn, block);
+          if (c < N && column(rw.code(c), rp, rn, rD, rb) == block) { hp = ~0ULL; hn = 0ULL; }
+          bp = (int)(hp >> offset) & 1;
+          bn = (int)(hn >> offset) & 1;
         }
         const int t = bp ? 1 : bn == 0 ? 0 : 2;
         diff++;
@@ -2093,15 +2096,13 @@ struct BsfLane {
   // step or report touches is as it would be without the suspension.
   enum { LP_RUN = 0, LP_WAIT = 1, LP_FINISH = 2, LP_SUSPEND = 3 };
   int susPhase = LP_RUN;  // the phase a suspended read resumes in (LP_RUN or LP_WAIT: a report pending)
-  // room for one control round (controlPass) and the FM step it may end in, by where the round starts:
-  // a run-ahead (xMode 3) ends with at most one new state and one queue entry; a poll (0) is followed
-  // by a child (+1 state, +1 entry, the polled one gone) or the split and clip children (+4 states, +2
-  // entries); the choice of a child (1) by a child or the split children; the split stage (2) by
-  // those.  0 when there is room, else the OV_* capacity that may run out.
+  // room for one micro-step (searchStep), by where it starts: at most 5 new states (a child, then the
+  // split and clip children's 4 when it was the last candidate; or a first child and its run-ahead's
+  // last state) and, net of a poll (xMode 0), 2 more queue entries; 3 from the next child (1).  0 when
+  // there is room, else the OV_* capacity that may run out.
   GWA_HD int passRoom() const {
-    const int a = xMode == 3 ? 1 : 4;
-    const int q = xMode == 3 ? 1 : xMode == 0 ? 1 : 2;
-    return nStates + a > caps.arena ? OV_ARENA : heapSize + q > caps.heap ? OV_HEAP : 0;
+    const int q = xMode == 1 ? 3 : 2;
+    return nStates + 5 > caps.arena ? OV_ARENA : heapSize + q > caps.heap ? OV_HEAP : 0;
   }
   GWA_HD int laneStep() {
     const int st = searchStep();
@@ -2142,19 +2143,16 @@ struct BsfLane {
   // no record for read r at rec (restart on the next tier)
   GWA_HD static void resumeInvalidate(uint8_t *rec) { ((uint32_t *)rec)[0] = 0; }
   GWA_HD void suspendTo(uint8_t *rec, uint32_t r) {
-    int32_t v[kResumeInts] = {};
-    int q = 1;  // (v[0]: the magic word, written last)
-    v[q++] = (int32_t)r;
-    v[q++] = minMismatches; v[q++] = maxMatchLength; v[q++] = bestScore; v[q++] = numFMIndexSearches;
-    v[q++] = nStates; v[q++] = heapSize; v[q++] = nHits; v[q++] = listSize; v[q++] = nCigar; v[q++] = listOk;
-    v[q++] = pendingBase; v[q++] = upperSearches; v[q++] = xMode; v[q++] = xT; v[q++] = xBase; v[q++] = xC;
-    v[q++] = xNm; v[q++] = xNextBase; v[q++] = xFirst; v[q++] = raIt; v[q++] = raMoved; v[q++] = raNs;
-    v[q++] = cacheIdx; v[q++] = cacheDirty; v[q++] = susPhase;
-    v[q++] = quickSteps; v[q++] = blocks; v[q++] = saReads; v[q++] = maxHeap; v[q++] = kmerLookups;
-    v[q++] = shortSteps; v[q++] = textSteps; v[q++] = textRuns; v[q++] = numSW; v[q++] = verifyBytes;
     int32_t *h = (int32_t *)rec;
-    for (int i = 1; i < kResumeInts; ++i) h[i] = v[i];
-    *(uint64_t *)(rec + kResumeInts * 4) = raBound;
+    int q = 1;  // (h[0]: the magic word, written last)
+    h[q++] = (int32_t)r;
+    h[q++] = minMismatches; h[q++] = maxMatchLength; h[q++] = bestScore; h[q++] = numFMIndexSearches;
+    h[q++] = nStates; h[q++] = heapSize; h[q++] = nHits; h[q++] = listSize; h[q++] = nCigar; h[q++] = listOk;
+    h[q++] = pendingBase; h[q++] = upperSearches; h[q++] = xMode; h[q++] = xT; h[q++] = xBase; h[q++] = xC;
+    h[q++] = xNm; h[q++] = xNextBase;
+    h[q++] = cacheIdx; h[q++] = cacheDirty; h[q++] = susPhase;
+    h[q++] = quickSteps; h[q++] = blocks; h[q++] = saReads; h[q++] = maxHeap; h[q++] = kmerLookups;
+    h[q++] = shortSteps; h[q++] = textSteps; h[q++] = textRuns; h[q++] = numSW; h[q++] = verifyBytes;
     *(DState<R> *)(rec + kResumeInts * 4 + 8) = cache;
     uint8_t *o = rec + resumeHdrBytes();
     copyOut(o, (const uint8_t *)L.arena(), sizeof(DState<R>) * (size_t)nStates);
@@ -2171,19 +2169,22 @@ struct BsfLane {
     for (int i = 0; i < nCigar; ++i) co[i] = L.cigar()[i];
     h[0] = (int32_t)kResumeMagic;  // (written last: the record is complete)
   }
-  // true when rec holds read r's suspended search; then the lane continues it (phase in *phase)
-  GWA_HD bool resumeFrom(const uint8_t *rec, uint32_t r, int *phase) {
+  GWA_HD static bool resumeValid(const uint8_t *rec, uint32_t r) {
     const int32_t *h = (const int32_t *)rec;
-    if ((uint32_t)h[0] != kResumeMagic || (uint32_t)h[1] != r) return false;
+    return (uint32_t)h[0] == kResumeMagic && (uint32_t)h[1] == r;
+  }
+  // true when rec holds read r's suspended search; then the lane continues it (phase in *phase)
+  GWA_HD bool resumeFrom(const uint8_t *rec, uint32_t r, int *phase, bool masks = true) {
+    const int32_t *h = (const int32_t *)rec;
+    if (!resumeValid(rec, r)) return false;
     int q = 2;
     minMismatches = h[q++]; maxMatchLength = h[q++]; bestScore = h[q++]; numFMIndexSearches = h[q++];
     nStates = h[q++]; heapSize = h[q++]; nHits = h[q++]; listSize = h[q++]; nCigar = h[q++]; listOk = h[q++];
     pendingBase = h[q++]; upperSearches = h[q++]; xMode = h[q++]; xT = h[q++]; xBase = h[q++]; xC = h[q++];
-    xNm = h[q++]; xNextBase = h[q++]; xFirst = h[q++]; raIt = h[q++]; raMoved = h[q++]; raNs = h[q++];
+    xNm = h[q++]; xNextBase = h[q++];
     cacheIdx = h[q++]; cacheDirty = h[q++]; *phase = h[q++];
     quickSteps = h[q++]; blocks = h[q++]; saReads = h[q++]; maxHeap = h[q++]; kmerLookups = h[q++];
     shortSteps = h[q++]; textSteps = h[q++]; textRuns = h[q++]; numSW = h[q++]; verifyBytes = h[q++];
-    raBound = *(const uint64_t *)(rec + kResumeInts * 4);
     cache = *(const DState<R> *)(rec + kResumeInts * 4 + 8);
     const uint8_t *o = rec + resumeHdrBytes();
     copyOut((uint8_t *)L.arena(), o, sizeof(DState<R>) * (size_t)nStates);
@@ -2198,7 +2199,7 @@ struct BsfLane {
     o += ((size_t)listSize * 4 + 15) & ~(size_t)15;
     const uint16_t *co = (const uint16_t *)o;
     for (int i = 0; i < nCigar; ++i) L.cigar()[i] = co[i];
-    buildMasks();  // the read words / QueryMask rows in LDS (searchStart builds them on a fresh start)
+    if (masks) buildMasks();  // the read words / QueryMask rows in LDS (searchStart builds them on a fresh start)
     status = ST_UNMAPPED;
     ovfWhat = 0;
     return true;
@@ -2207,9 +2208,9 @@ struct BsfLane {
   GWA_HD static void copyOut(uint8_t *dst, const uint8_t *src, size_t n) {
     for (size_t i = 0; i < n / 8; ++i) ((uint64_t *)dst)[i] = ((const uint64_t *)src)[i];
   }
-  GWA_HD bool searchStart(const ScanRes &sr) {
+  GWA_HD bool searchStart(const ScanRes &sr, bool masks = true) {
     GWA_PT(tsd);
-    buildMasks();
+    if (masks) buildMasks();
     int a = -1, b = -1;
     if (sr.nmF <= k) {
       if (sr.lmF != 0 && sr.lmF < m) a = newInitial(0, D_BIFWD, 0, m, sr.lmF, sr.lmF, sr.nmF);
@@ -2227,44 +2228,27 @@ struct BsfLane {
     upperSearches = m * 20;
     return true;
   }
-  // One call = one micro-step of the loop of align_internal (:343-477) with at most ONE FM step, and
-  // that step at ONE call site (buildChild below): every lane of a wavefront that has an FM step to
-  // take in this call takes it there together, whichever part of the loop it came from -- the child
-  // of a poll (xMode 1), or the next step of a run-ahead (xMode 3).  The control work before it
-  // (poll, pruning, the choice of the child, the split / clip children) runs per lane for up to
-  // two rounds (controlPass), so a lane whose poll ends in a prune or a split still reaches the FM step
-  // of this call.  Nothing else touches a lane between its micro-steps, so the order of operations on its
-  // heap and arena is exactly the reference's.
+  // One call = one micro-step of the loop of align_internal (:343-477).  A poll is followed by at
+  // most ONE child expansion (an FM step); the remaining children of the same poll and the split /
+  // clip children come in later calls (xMode 1 / 2), so every lane of a wavefront performs about
+  // one FM step per call instead of the wavefront looping until its slowest lane has tried all
+  // four bases.  Nothing else touches a lane between its micro-steps, so the order of operations
+  // on its heap and arena is exactly the reference's.
   // (the expanded state xC is re-read from the arena / cache at each micro-step rather than kept
   // in the lane object: its flag word is always stored, so the arena copy is current)
-  int xMode = 0, xT = 0, xBase = 0, xC = 0, xNm = 0, xNextBase = 0, xFirst = 0;
-  // run-ahead (xMode 3): the queue's bound (heapNoop), steps taken, whether the cached state moved,
-  // the run's first state
-  uint64_t raBound = 0;
-  int raIt = 0, raMoved = 0, raNs = -1;
-  // one round of the control work of a micro-step (searchStep): CP_STEP when it ends at an FM step
-  // (its parent in P, its base in ch), CP_AGAIN when it ended without one (a prune, the split / clip
-  // children, the end of a run-ahead), else CP_DONE / CP_REPORT
-  enum { CP_AGAIN = 0, CP_STEP = 1, CP_DONE = 2, CP_REPORT = 3 };
-  GWA_HD int controlPass(DState<R> &P, int &ch, int &kind) {
-    if (xMode == 3) {
-      const int nb = raNext();
-      if (nb >= 0) {  // the next step of the run (the checks of :352-396 passed for the cached state)
-        P = cache;
-        ch = nb;
-        kind = 2;
-        return CP_STEP;
-      }
-      const int ns = raFinish();
-      if (ns == -2) return CP_DONE;
-      queueAdd(update(xBase, xC, ns));
-      xMode = 0;
-      return CP_AGAIN;
+  int xMode = 0, xT = 0, xBase = 0, xC = 0, xNm = 0, xNextBase = 0;
+  GWA_HD int searchStep() {
+    // a micro-step starts only when it cannot overflow the arena or the queue (passRoom); else the
+    // read is suspended here, before it (suspend / resume below)
+    if (const int ov = passRoom()) {
+      ovfWhat |= ov;
+      return SS_SUSPEND;
     }
     DState<R> xCS;
     if (xMode == 0) {
-      if (!(heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR)) return CP_DONE;
-      if (numFMIndexSearches > upperSearches) return CP_DONE;
+      GWA_PC(PR_NSW, PR_NSL);
+      if (!(heapSize > 0 && status != ST_OVERFLOW && status != ST_ERROR)) return SS_DONE;
+      if (numFMIndexSearches > upperSearches) return SS_DONE;
       GWA_PT(tp);
       const int base = queuePoll();
       if (base != cacheIdx) flushCache();  // the deferred state stays queued
@@ -2285,14 +2269,14 @@ struct BsfLane {
       if ((((uint32_t)C.state >> 24) & 3) != 0 || cRemaining(C) == 0) {
         flushCache();  // verify reads the chain from the arena
         pendingBase = base;
-        return CP_REPORT;
+        return SS_REPORT;
       }
       // the checks below drop the polled state (a deferred one is chain-free: dead from here)
       const int nm = (int)(((uint32_t)C.state >> 8) & 0xFF);
       if ((C.state & 0x1F) == 0x1F || nm > minMismatches || minMismatches - nm < 0 || ubScore < 0 ||
           ubScore < bestScore) {  // isFinished / pruned
         dropIfCached(base);
-        return CP_AGAIN;
+        return SS_CONTINUE;
       }
       xBase = base;
       xC = c;
@@ -2307,28 +2291,47 @@ struct BsfLane {
     if (xMode == 1) {
       // children (:386-410): nextBase first -- a state from it ends the iteration -- then every
       // base still unchecked; one FM step per call
+      GWA_PT(te);
       // (the checked flags are stored once, with the child taken below or with the split flag: nothing
       // reads the arena copy of xC in between, siIsEmpty reads the register copy)
-      int c2 = -1, tt = xT, zero = 0;
-      for (; tt < 4 && c2 < 0; ++tt) {
+      int ch = -1, tt = xT, zero = 0;
+      for (; tt < 4 && ch < 0; ++tt) {
         zero |= tt == 0 ? 1 : 0;  // (single-exit loop, integer state: see quickScan)
         const int cand = tt < 0 ? xNextBase : tt;
         if (xCS.state & (1 << cand)) continue;  // isChecked
         xCS.state |= 1 << cand;                 // updateFlag
         if (siIsEmpty(xCS, cand)) continue;
-        c2 = cand;
+        ch = cand;
       }
       // StaircaseFilter sf = getStairCaseFilter(m) where the loop over every base begins (:439); this
       // micro-step entered it if it ran the loop at tt = 0
-      if (zero && !stairOk()) return CP_DONE;
-      xFirst = (xT < 0 && tt == 0) ? 1 : 0;  // the child taken is nextBase
+      if (zero && !stairOk()) return SS_DONE;
+      const int first = (xT < 0 && tt == 0) ? 1 : 0;  // the child taken is nextBase
       xT = tt;
-      if (c2 >= 0) {
+      if (ch >= 0) {
         storeStateWord(xC, xCS.state);
-        P = xCS;
-        ch = c2;
-        kind = 1;
-        return CP_STEP;
+        GWA_PT(tn);
+        int ns = nextStateLocal(xC, xCS, ch, first && xC == xBase && deferrable(xCS));
+        GWA_PA(PR_LOOP, tn);
+        if (ns == -2) return SS_DONE;
+        if (ns >= 0) {
+          if (first && xC == xBase) {
+            GWA_PT(tra);
+            ns = runAhead(ns);
+            GWA_PA(PR_BOUND, tra);
+            if (ns == -2) return SS_DONE;
+          }
+          GWA_PT(tad);
+          queueAdd(update(xBase, xC, ns));
+          GWA_PA(PR_ADD1, tad);
+          if (first) {
+            xMode = 0;
+            GWA_PA(PR_EXP1, te);
+            return SS_CONTINUE;
+          }
+        }
+        GWA_PA(PR_EXPN, te);
+        if (xT < 4) return SS_CONTINUE;  // more candidates: next call
       }
       xMode = 2;
     }
@@ -2344,7 +2347,7 @@ struct BsfLane {
         for (int clip = 0; clip < 2; ++clip) {  // split, then clip (:414-425)
           uint64_t key = 0;
           const int ns = nextStateAfterSplit(xCS, clip != 0, &key);
-          if (ns == -2) return CP_DONE;
+          if (ns == -2) return SS_DONE;
           if (ns >= 0) {
             if (xC == xBase) queueAddKeyed((key << KS) | (uint64_t)ns);  // update(base, base, ns) == ns
             else queueAdd(update(xBase, xC, ns));
@@ -2354,74 +2357,6 @@ struct BsfLane {
     }
     if (xC == xBase && deferrable(xCS)) dropIfCached(xC);  // the expanded chain-free state is done
     GWA_PA(PR_SPLIT, ts);
-    return CP_AGAIN;
-  }
-  GWA_HD int searchStep() {
-    DState<R> P;  // the parent of this call's FM step (a register copy)
-    int ch = -1, kind = 0;  // the FM step's base; kind 1: a child of xC, 2: a run-ahead step
-    GWA_PC(PR_NSW, PR_NSL);
-    // two rounds of control work, written out (no loop: early exits from divergent loops have been
-    // mis-lowered on gfx950); a round starts only when it cannot overflow the
-    // arena or the queue (passRoom), else the read is suspended here (before the first) or the call
-    // ends (before the second)
-    if (const int ov = passRoom()) {
-      ovfWhat |= ov;
-      return SS_SUSPEND;
-    }
-    int cp = controlPass(P, ch, kind);
-    if (cp == CP_AGAIN && passRoom() == 0) cp = controlPass(P, ch, kind);
-    if (cp == CP_DONE) return SS_DONE;
-    if (cp == CP_REPORT) return SS_REPORT;
-    if (cp != CP_STEP) return SS_CONTINUE;
-    const int fm0 = numFMIndexSearches, ts0 = textSteps;
-    // ---- the FM step of this call: next(c, ch) and the automaton step, SearchState.nextState ----
-    GWA_PT(tn);
-    DState<R> d;
-    const bool ok = buildChild(P, ch, d);
-    GWA_PA(PR_LOOP, tn);
-    if (kind == 2) {  // run-ahead
-      if (!ok) {  // a rejected first child: the state goes through the loop as the reference runs it
-        numFMIndexSearches = fm0;
-        textSteps = ts0;
-        raIt = cfg.runAheadMax;  // the run ends at the next call
-      } else {
-        cache = d;
-        raMoved = 1;
-        ++raIt;
-      }
-      return SS_CONTINUE;
-    }
-    // a child of xC (nextStateLocal): in a new arena slot, cached.  When xC is the polled chain-free
-    // state and this child is its accepted next base, the reference drops xC: a deferred xC is not
-    // written back
-    int ns = -1;
-    if (ok) {
-      const int id = allocState();
-      if (id < 0) return SS_DONE;
-#ifndef GWA_NO_CACHE
-      if (xFirst && xC == xBase && deferrable(P) && xC == cacheIdx) cacheDirty = 0;
-      flushCache();
-      cache = d;
-      cacheIdx = id;
-      if (deferrable(d)) cacheDirty = 1;
-      else { GWA_PW(PR_WA, PR_EA, sizeof(DState<R>)); L.arena()[id] = d; }
-#else
-      L.arena()[id] = d;
-#endif
-      ns = id;
-    }
-    if (ns >= 0) {
-      if (xFirst && xC == xBase && raStart(ns)) {  // its next steps run ahead (xMode 3)
-        xMode = 3;
-        return SS_CONTINUE;
-      }
-      queueAdd(update(xBase, xC, ns));
-      if (xFirst) {
-        xMode = 0;
-        return SS_CONTINUE;
-      }
-    }
-    if (xT >= 4) xMode = 2;  // no candidate left: the split / clip children next
     return SS_CONTINUE;
   }
 
@@ -2516,6 +2451,27 @@ struct BsfLane {
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nh ? rows[i] : 0;
     return true;
   }
+  // the child in a new arena slot (stays cached); -1 null, -2 overflow.  parentDead: c is the
+  // polled chain-free state and this child is its accepted next base (the reference drops c), so a
+  // deferred c is not written back
+  GWA_HD int nextStateLocal(int c, const DState<R> &cs, int ch, bool parentDead) {
+    DState<R> d;
+    if (!buildChild(cs, ch, d)) return -1;
+    int id = allocState();
+    if (id < 0) return -2;
+#ifndef GWA_NO_CACHE
+    if (parentDead && c == cacheIdx) cacheDirty = 0;
+    flushCache();
+    cache = d;
+    cacheIdx = id;
+    if (deferrable(d)) cacheDirty = 1;
+    else { GWA_PW(PR_WA, PR_EA, sizeof(DState<R>)); L.arena()[id] = d; }
+#else
+    L.arena()[id] = d;
+#endif
+    return id;
+  }
+
   // ---- run-ahead over text-mode match runs ----
   // When the polled state's first child (its own next base, :386-396) is accepted, the reference
   // pushes it and ends the iteration; the next poll usually returns that child, whose first child
@@ -2558,38 +2514,44 @@ struct BsfLane {
   GWA_HD uint64_t keyOfLocal(const DState<R> &c) const {  // keyOf of a chain-free state
     return packKey((int)(((uint32_t)c.state >> 16) & 0xFF), stateScore(c, 0, false), cProcessed(c));
   }
-  // a run starts from the child ns just created (cached) when the queue provably comes back unchanged
-  GWA_HD bool raStart(int ns) {
-    if (cfg.runAheadMax <= 0 || cacheIdx != ns || cache.nextSplit >= 0 || !siText(cache)) return false;
-    if (!heapNoop(&raBound)) return false;
-    raIt = 0;
-    raMoved = 0;
-    raNs = ns;
-    return true;
-  }
-  // the loop top (:352-356) and the poll checks (:358-396) for the cached state: its next base, or -1
-  // when the run ends here
-  GWA_HD int raNext() {
-    if (raIt >= cfg.runAheadMax) return -1;
-    if (numFMIndexSearches > upperSearches || status == ST_OVERFLOW || status == ST_ERROR) return -1;
-    if (keyOfLocal(cache) >= raBound) return -1;
-    if ((((uint32_t)cache.state >> 24) & 3) != 0 || cRemaining(cache) == 0) return -1;
-    if ((cache.state & 0x1F) == 0x1F) return -1;
-    const int nm = (int)(((uint32_t)cache.state >> 8) & 0xFF);
-    if (nm > minMismatches) return -1;
-    const int ubs = stateScore(cache, 0, true);
-    if (ubs < 0 || ubs < bestScore) return -1;
-    if (!siText(cache)) return -1;
-    const int nb = qcode(cStrand(cache), cNextIdx(cache));
-    // (the parent's checked flag for nb is not recorded: the parent is never read again, and the
-    // child takes only the priority bits of the parent's state word)
-    if ((cache.state & (1 << nb)) != 0 || siIsEmpty(cache, nb)) return -1;
-    return nb;
-  }
-  // the run's end: its last state takes the place of the first (raNs, never referenced) in the queue;
-  // -2 overflow
-  GWA_HD int raFinish() {
-    if (!raMoved) return raNs;
+  GWA_HD int runAhead(int ns) {
+#ifdef GWA_NO_RA
+    return ns;
+#endif
+    if (cfg.runAheadMax <= 0 || cacheIdx != ns || cache.nextSplit >= 0 || !siText(cache)) return ns;
+    uint64_t bound;
+    if (!heapNoop(&bound)) return ns;
+    // the run works on the register copy `cache` (the state to be polled next) in place
+    int moved = 0;
+    for (int it = 0; it < cfg.runAheadMax; ++it) {
+      // loop top (:352-356) and the poll checks (:358-385) for the cached state
+      if (numFMIndexSearches > upperSearches || status == ST_OVERFLOW || status == ST_ERROR) break;
+      if (keyOfLocal(cache) >= bound) break;
+      if ((((uint32_t)cache.state >> 24) & 3) != 0 || cRemaining(cache) == 0) break;
+      if ((cache.state & 0x1F) == 0x1F) break;
+      const int nm = (int)(((uint32_t)cache.state >> 8) & 0xFF);
+      if (nm > minMismatches) break;
+      const int ubs = stateScore(cache, 0, true);
+      if (ubs < 0 || ubs < bestScore) break;
+      if (!siText(cache)) break;
+      const int nb = qcode(cStrand(cache), cNextIdx(cache));
+      if ((cache.state & (1 << nb)) != 0 || siIsEmpty(cache, nb)) break;
+      // (the parent's checked flag for nb is not recorded: the parent is never read again, and the
+      // child takes only the priority bits of the parent's state word)
+      DState<R> d;
+      const int fm0 = numFMIndexSearches, ts0 = textSteps;
+      const bool ok = buildChild(cache, nb, d);
+      if (!ok) {  // a rejected first child: the state goes through the loop as the reference runs it
+        numFMIndexSearches = fm0;
+        textSteps = ts0;
+        break;
+      }
+      cache = d;
+      moved = 1;
+    }
+    if (!moved) return ns;
+    // ns (the run's first state, deferred or written) is never referenced: the run's last state
+    // takes its place in the queue
     const int id = allocState();
     if (id < 0) return -2;
     cacheDirty = 0;

@@ -58,7 +58,9 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
 #ifndef GWA_SEARCH_WAVES
 #define GWA_SEARCH_WAVES 2
 #endif
-template <int R, int QW, int LH>
+// RES: the tier may resume reads from records (tiers >= 1; the first tier only suspends: the resume
+// path's register pressure is kept out of the kernel that runs most reads)
+template <int R, int QW, int LH, bool RES>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES))) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
                                                          const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                                                          uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
@@ -121,7 +123,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   // Persistent lanes with a shared read counter.  A lane whose search reaches a report parks (WAIT);
   // the wavefront runs the parked reports (DP verification + traceback) together once they are at
   // least half of its live lanes, instead of once per lane on a divergent path.
-  enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED, SUSPEND };
+  enum { IDLE, RUN, WAIT, FINISH, EXHAUSTED, SUSPEND, RESUME };
+  uint32_t resIdx = 0;
   int phase = IDLE;
   uint32_t r = 0;
   // deep tiers with few reads (caps.sparse > 1): only every caps.sparse-th lane takes reads, so the
@@ -146,18 +149,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
           lane.trace = nullptr;
           if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; lane.traceN = 0; }
           lane.initRead(reads.codes + o, m);
-          // a read the previous tier suspended continues from its record (Lane::resumeFrom)
-          int rp = 0;
-          if (res.in && i < res.inCap && lane.resumeFrom(res.in + (size_t)i * res.inStride, r, &rp))
-            phase = rp == Lane::LP_WAIT ? WAIT : RUN;
-          else
-            phase = lane.searchStart(sres[r]) ? RUN : FINISH;
+          // a read the previous tier suspended continues from its record (Lane::resumeFrom, below)
+          lane.buildMasks();
+          const bool rec = RES && res.in && i < res.inCap && lane.resumeValid(res.in + (size_t)i * res.inStride, r);
+          if (rec) {
+            resIdx = i;
+            phase = RESUME;
+          } else {
+            phase = lane.searchStart(sres[r], false) ? RUN : FINISH;
+          }
         } else {
           phase = EXHAUSTED;
         }
       }
     }
     if (__ballot(phase != EXHAUSTED) == 0) break;
+    if (RES && phase == RESUME) {
+      int rp = 0;
+      lane.resumeFrom(res.in + (size_t)resIdx * res.inStride, r, &rp, false);
+      phase = rp == Lane::LP_WAIT ? WAIT : RUN;
+    }
     const int nWait = __popcll(__ballot(phase == WAIT));
     const int nRun = __popcll(__ballot(phase == RUN));
 #ifdef GWA_PROF
@@ -291,12 +302,13 @@ void launchSearchQR(int ldsHeap, uint32_t lanes, const IndexView &ix, const Sear
                     uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, const ResumeBufs &res,
                     hipStream_t s, uint32_t *trace, int traceRead) {
   dim3 grid((lanes + 255) / 256);
-#define GWA_CASE(LL)                                                                                                   \
-  hipLaunchKernelGGL((bsf_search_kernel<R, QW, LL>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n, scratch,  \
-                     laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, res, trace, traceRead)
-  if (ldsHeap == 2) GWA_CASE(2);
-  else if (ldsHeap) GWA_CASE(1);
-  else GWA_CASE(0);
+#define GWA_CASE(LL, RR)                                                                                               \
+  hipLaunchKernelGGL((bsf_search_kernel<R, QW, LL, RR>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
+                     scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, res, trace, traceRead)
+  if (ldsHeap == 2) GWA_CASE(2, true);
+  else if (ldsHeap && res.in) GWA_CASE(1, true);
+  else if (ldsHeap) GWA_CASE(1, false);
+  else GWA_CASE(0, true);
 #undef GWA_CASE
 }
 
