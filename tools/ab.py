@@ -85,7 +85,8 @@ def main():
             for k in envs.get(i, {}):
                 del os.environ[k]
             if rep > 0:
-                times[p].append((dt * 1e3, st.encode_ms, st.quickscan_ms, st.search_ms, st.format_ms, list(st.tier_ms)))
+                times[p].append((dt * 1e3, st.encode_ms, st.quickscan_ms, st.search_ms, st.format_ms, list(st.tier_ms),
+                                 list(st.tier_reads)))
     ref = None
     rng = np.random.default_rng(5)
     samp = np.sort(rng.choice(n, min(n, 200000), replace=False)).astype(np.uint32)
@@ -95,9 +96,10 @@ def main():
         sam, _ = b.results_select(samp)
         same = "ref" if ref is None else (sam == ref)
         ref = ref if ref is not None else sam
-        say("%-40s step %.1f ms (median of %d) = %.2f M reads/s; encode %.2f qs %.2f search %.2f format %.2f tiers %s; SAM %s"
+        say("%-40s step %.1f ms (median of %d) = %.2f M reads/s; encode %.2f qs %.2f search %.2f format %.2f tiers %s "
+            "(reads %s); SAM %s"
             % (os.path.basename(p) + str(envs.get(i, "")), med, len(ts), n / med / 1e3, ts[-1][1], ts[-1][2], ts[-1][3],
-               ts[-1][4], [round(x, 1) for x in ts[-1][5]], same))
+               ts[-1][4], [round(x, 1) for x in ts[-1][5]], ts[-1][6], same))
 
 
 if __name__ == "__main__":
