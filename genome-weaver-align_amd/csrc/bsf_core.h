@@ -223,6 +223,7 @@ struct Caps {
   int32_t cand;  // SuffixFilter candidate set (sf_core.h); 0 on the BSF path
   int32_t sparse;  // > 1: only every sparse-th lane of a wavefront takes reads (deep tiers, bsf_search_kernel)
   int32_t sf;      // 1: the arena holds SfState<R> (sf_core.h), else DState<R>
+  int32_t spec;    // -m sf sparse last tier: speculative verification results (SfLane::SpecEntry, a power of two)
 };
 // bytes of one arena slot: SfState<R> is 24 + 8 R bytes (static_assert in sf_core.h)
 template <int R>
@@ -237,7 +238,7 @@ struct LaneMem {
   // two base pointers + uniform offsets (kept in SGPRs), not eight per-lane pointers
   uint8_t *slice;          // this lane's slice: arena | heap | hits | list | cigar
   uint8_t *chunk;          // interleaved block (the wavefront's on the GPU, the lane's on the host)
-  uint32_t oHeap, oCand, oHits, oList, oCigar;  // byte offsets in the slice
+  uint32_t oHeap, oCand, oHits, oList, oCigar, oSpec;  // byte offsets in the slice
   uint32_t oPath;          // byte offset of the path plane in the chunk
   int lane, is;            // lane in the interleaved block, interleave stride (elements)
   // PriorityQueue array of (key << KS | state index): entry i at heapP[i * hs].  In the slice
@@ -267,6 +268,7 @@ GWA_HD size_t laneBytes(const Caps &c) {  // per-lane slice
   b += sizeof(DHit) * (size_t)c.hits;
   b += 4 * (size_t)c.list;
   b += 2 * (size_t)c.cigar;
+  if (c.spec > 0) b = ((b + 63) & ~(size_t)63) + 64 * (size_t)c.spec;
   return (b + 255) & ~(size_t)255;
 }
 GWA_HD size_t ilvBytes(const Caps &c) {  // interleaved bytes per lane
@@ -284,7 +286,8 @@ GWA_HD LaneMem<R> laneMem(uint8_t *slice, uint8_t *chunk, int laneInWave, int is
   L.oCand = (uint32_t)b; b += 8 * (size_t)c.cand;
   L.oHits = (uint32_t)b; b += sizeof(DHit) * (size_t)c.hits;
   L.oList = (uint32_t)b; b += 4 * (size_t)c.list;
-  L.oCigar = (uint32_t)b;
+  L.oCigar = (uint32_t)b; b += 2 * (size_t)c.cigar;
+  L.oSpec = (uint32_t)((b + 63) & ~(size_t)63);
   L.chunk = chunk;
   L.oPath = (uint32_t)((size_t)is * 8 * (size_t)c.dpWords);
   L.lane = laneInWave;
@@ -381,7 +384,13 @@ struct Overflow {};  // thrown only on host test builds; device uses status code
 // DP then needs at most DB = QW / 2 blocks of 64 rows.  HY: hybrid heap (hslot).
 // KS: bits of the state index in a queue entry (key << KS | index).  Both paths' keys are 40 bits
 // (packKey here, SfLane::keyOf), so an arena holds up to 2^24 states.
-template <int R, int QW = 8, bool HY = false, int KS = 24>
+// DPM: the DP traceback's history (alignBlockDetailed): 0 = column checkpoints, recomputed on
+// demand; 1 = the first tier's kernel, whose reads of more than two 64-row blocks keep a 32-row
+// slice of every column instead (the recompute of a 4-block column costs the k >= 4 first tier more
+// than the slice's 8 B per column); 2 = every column's blocks (16 B per block per column: the -m sf
+// verification of a lone lane, whose tracebacks take tens of edits and would recompute a column
+// per edit)
+template <int R, int QW = 8, bool HY = false, int KS = 24, int DPM = 0>
 struct BsfLane {
   static constexpr int DB = QW / 2;
   static constexpr uint64_t IDXM = (1ULL << KS) - 1ULL;
@@ -1361,12 +1370,9 @@ struct BsfLane {
   }
 
   // BitParallelSmithWaterman.alignBlockDetailed (A/BitParallelSmithWaterman.java:141-147,394-644).
-  // The live column (<=4 blocks of 64 rows) stays in VGPRs.  The vp/vn history the traceback needs
-  // goes to HBM scratch as one 16-B {vp, vn} pair per (column, block) -- one dwordx4 store per block
-  // per column, 64 lanes of a wavefront adjacent -- and the per-column write record (bits 0-3
-  // computed, 4-7 activated-as-input; cells never written read as 0, as the reference's
-  // zero-initialised long[][] do) is packed 4 columns to a u32 and stored once per 4 columns.
-  struct alignas(16) VpVn { uint64_t vp, vn; };
+  // The live column (<= DB blocks of 64 rows) stays in VGPRs; the history the traceback reads is
+  // kept in the lane's interleaved DP area (64 lanes of a wavefront adjacent per word) as column
+  // checkpoints or, in the first tier's k >= 4 kernel, a 32-row slice per column (DPM, below).
   // bits [lo, lo + 32) of a DP column of DB blocks (rows outside [0, 64 DB) read as 0)
   GWA_HD static uint32_t rows32(const uint64_t (&E)[DB], int lo) {
     const int w = lo >> 6, sh = lo & 63;  // lo < 0: w = -1
@@ -1388,8 +1394,10 @@ struct BsfLane {
     return rows >= 64 ? x : (x & ((1ULL << rows) - 1ULL));
   }
   // returns 0 ok, 1 null (no alignment), <0 overflow
+  // cgOver / capOver: the CIGAR area and its capacity, when not the lane's own (the helper lanes of
+  // the cooperative -m sf kernel, whose slice is the owner's)
   GWA_HD int alignBlockDetailed(int strand, int qs, int qe, int64_t refStart, int64_t refEnd, int *outPos, int *outDiff,
-                                int *cigOff, int *cigLen) {
+                                int *cigOff, int *cigLen, uint16_t *cgOver = nullptr, int capOver = 0) {
     const int w = 64;
     const int mq = qe - qs;
     const int kb = cfg.bandWidth;
@@ -1475,9 +1483,21 @@ struct BsfLane {
     // at chunk[e * is + lane]; the traceback recomputes the column an edit needs from the checkpoint at
     // or before it (below).  ~6 words per 16 columns instead of one word per column (first tier) or
     // 16 B per block per column (deeper tiers), and no traceback ever leaves the kept rows.
+    // DPM 1 with more than two blocks: one word per column instead, rows [lo, lo + 32) of column j + 1
+    // with lo = j - c0 - 16 -- the diagonal band a k <= 15 traceback of a first-tier read stays in;
+    // one that leaves it overflows (OV_SLICE: laneReport rolls the report back and the read resumes
+    // on the next tier, whose kernel keeps checkpoints).  Activated rows (~0 / 0) are patched into
+    // the previous column's word.
+    constexpr bool kSlice = DPM == 1 && DB > 2;
+    constexpr bool kHist = DPM == 2;
+    struct alignas(16) VpVn { uint64_t vp, vn; };
+    VpVn *hist = (VpVn *)L.chunk + L.lane;  // DPM 2: {vp, vn} of block b of column c at [(c * bMax + b) * is]
+    const int c0 = ((N - mq) >> 1) + (caps.dpSlice > 0 ? caps.dpSlice - 1 : 0);
+    uint64_t *h8 = (uint64_t *)L.chunk + L.lane;
+    uint64_t lastWord = 0;
     constexpr int kCk = 16, kCw = 2 * DB + (DB + 2) / 2;  // checkpoint words
     uint64_t *ckBase = (uint64_t *)L.chunk + L.lane;
-    if ((size_t)((N + kCk - 1) / kCk + 1) * kCw > (size_t)caps.dpWords) { ovf(OV_DP); return -1; }
+    if (!kSlice && !kHist && (size_t)((N + kCk - 1) / kCk + 1) * kCw > (size_t)caps.dpWords) { ovf(OV_DP); return -1; }
     auto ckStore = [&](int t) {
       uint64_t *e = ckBase + (size_t)t * kCw * is;
 #pragma unroll
@@ -1500,8 +1520,29 @@ struct BsfLane {
       const int ch = (runN & 1ULL) ? 4 : (int)(run2 & 3ULL);
       run2 >>= 2;
       runN >>= 1;
-      if ((j & (kCk - 1)) == 0) ckStore(j / kCk);  // the state entering column j
-      column(ch, vp, vn, D, bCeil);
+      if (!kSlice && !kHist && (j & (kCk - 1)) == 0) ckStore(j / kCk);  // the state entering column j
+      const int actBlock = column(ch, vp, vn, D, bCeil);
+      if (kHist) {  // column j + 1; a block activated with input column j reads ~0 / 0 there
+        VpVn *hc = hist + (size_t)j * bMax * is;
+        if (actBlock >= 0) hc[(size_t)actBlock * is] = VpVn{~0ULL, 0ULL};
+#pragma unroll
+        for (int r = 0; r < DB; ++r)
+          if (r < bMax) hc[((size_t)bMax + r) * is] = VpVn{vp[r], vn[r]};
+        GWA_PW(PR_WD, PR_ED, 16 * bMax);
+      }
+      if (kSlice) {
+        uint64_t *hc8 = h8 + (size_t)j * is;
+        if (actBlock >= 0) {
+          const int lo = j - c0 - 17, r0 = 64 * actBlock - lo, r1 = r0 + 64;
+          const int s0 = r0 < 0 ? 0 : r0 > 32 ? 32 : r0, s1 = r1 < 0 ? 0 : r1 > 32 ? 32 : r1;
+          const uint64_t msk = ((s1 >= 32 ? 0xFFFFFFFFULL : (1ULL << s1) - 1ULL) & ~((1ULL << s0) - 1ULL));
+          *hc8 = (lastWord | msk) & ~(msk << 32);
+        }
+        const int lo1 = j - c0 - 16;
+        lastWord = (uint64_t)rows32(vp, lo1) | ((uint64_t)rows32(vn, lo1) << 32);
+        hc8[is] = lastWord;
+        GWA_PW(PR_WD, PR_ED, 8);
+      }
       if (bCeil == bMax) {
         const int dl = pick(D, bCeil - 1);
         if (!have) { have = 1; bestTail = j; bestDiff = dl; continue; }
@@ -1510,7 +1551,6 @@ struct BsfLane {
     }
     GWA_PA(PR_DPF, tdf);
     (void)bestDiff;
-    (void)caps.dpSlice;  // (the first tier's DP slice is gone: checkpoints serve every tier)
     if (!have) return 1;
     GWA_PT(tdt);
     // Traceback (:515-643).  A match decides the step from the codes alone (:547), so the history is
@@ -1521,8 +1561,8 @@ struct BsfLane {
     // (`right`), S/I/D after the last M the leading one (`left`); the runs in between are kept
     // (generation order) at the top of this read's CIGAR area, CIGAR entry cap-1-i = run i.  The ops
     // then come out as cigarStr = reverse(path) + CIGAR.add merging would make them (:599-643).
-    uint16_t *cg = L.cigar();
-    const int cap = caps.cigar;
+    uint16_t *cg = cgOver ? cgOver : L.cigar();
+    const int cap = cgOver ? capOver : caps.cigar;
     int row = mq - 1, col = bestTail;
     int diff = 0, leftMostPos = 0;
     int right = 0, adj = 0;  // trailing S/I/D count, of which I/D
@@ -1582,8 +1622,18 @@ struct BsfLane {
         // the history the reference holds for column c = col + 1 (:532-546), recomputed: the value
         // column c - 1 computed, unless the block of this row was activated with input column c
         // (then ~0 / 0), from the checkpoint at or before column c - 1
-        int bp, bn;
-        {
+        int bp = 0, bn = 0;
+        if (kSlice) {
+          const int rr = row - (col + 1 - c0 - 17);
+          if (rr < 0 || rr >= 32) { ovf(OV_SLICE); return -1; }
+          const uint64_t h = h8[(size_t)(col + 1) * is];
+          bp = (int)(h >> rr) & 1;
+          bn = (int)(h >> (32 + rr)) & 1;
+        } else if (kHist) {
+          const VpVn h = hist[((size_t)(col + 1) * bMax + (row >> 6)) * is];
+          bp = (int)(h.vp >> (row & 63)) & 1;
+          bn = (int)(h.vn >> (row & 63)) & 1;
+        } else {
           const int c = col + 1, block = row >> 6, offset = row & 63;
           const int t = (c - 1) / kCk;
           uint64_t rp[DB], rn[DB];
@@ -1623,17 +1673,23 @@ struct BsfLane {
     if (bad) { ovf(OV_CIGAR); return -1; }
     GWA_PA(PR_DPT, tdt);
     const int off = nCigar;
+    auto put = [&](int type, int len) -> int {  // putCigarOp on this DP's CIGAR area
+      if (nCigar >= cap) { ovf(OV_CIGAR); return -1; }
+      GWA_PW(PR_WH, PR_EH, 2);
+      cg[nCigar++] = (uint16_t)((len << 3) | type);
+      return 0;
+    };
     if (!seenM) {
       diff -= adj;  // the whole path is the leading clip (left = plen, right = 0)
-      if (right > 0 && putCigarOp(4, right) < 0) return -1;
+      if (right > 0 && put(4, right) < 0) return -1;
     } else {
       if (nCigar + 2 * nRuns + 4 > cap) { ovf(OV_CIGAR); return -1; }
       cg[cap - 1 - nRuns] = (uint16_t)((curL << 3) | curT);
       GWA_PW(PR_WH, PR_EH, 2 * (lastM + 2));
       diff -= adj + pendAdj;
-      if (pendL > 0 && putCigarOp(4, pendL) < 0) return -1;
+      if (pendL > 0 && put(4, pendL) < 0) return -1;
       for (int i = lastM; i >= 0; --i) cg[nCigar++] = cg[cap - 1 - i];
-      if (right > 0 && putCigarOp(4, right) < 0) return -1;
+      if (right > 0 && put(4, right) < 0) return -1;
     }
     *cigOff = off;
     *cigLen = nCigar - off;

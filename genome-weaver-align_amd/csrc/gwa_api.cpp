@@ -932,10 +932,11 @@ static const Tier kTiers[kNumTiers] = {
     {65536, 65536, 4096, 4096, 65536, 0, 1024u},
 };
 // -m sf: no quick-scan exit, every read starts with up to 2 (k + 2) seeds; heap in the slice
+// (candidate sets of >= 64 slots are hash tables at most half full, SfLane::candInsert)
 static const Tier kSfTiers[kNumTiers] = {
     {512, 512, 32, 32, 512, 32, 128u * 1024u},
-    {2048, 2048, 64, 64, 2048, 256, 128u * 1024u},
-    {8192, 8192, 256, 256, 4096, 1024, 16384u},
+    {2048, 2048, 64, 64, 2048, 512, 128u * 1024u},
+    {8192, 8192, 256, 256, 4096, 2048, 16384u},
     {65536, 65536, 4096, 4096, 65536, 16384, 1024u},
 };
 
@@ -1106,6 +1107,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       }
       caps.cand = T.cand;
       caps.sf = sf ? 1 : 0;
+      caps.spec = 0;
       if (tb == kNumTiers - 1) {  // the grown last tier
         caps.arena <<= gArena;
         caps.heap <<= gArena;
@@ -1113,6 +1115,8 @@ int gwa_batch_run(gwa_batch_t *b) {
         caps.list <<= gList;
         caps.cigar <<= gCigar;
         caps.cand <<= gCand;
+        // -m sf: the speculation table of the cooperative kernel (run when the tier is sparse, 64)
+        if (sf) caps.spec = caps.cand;
       }
       // -m bsf, k >= 4 (R >= 8): the verification memo (bsf_core.h verify), twice the hit list's
       // entries, a power of two; k <= 3 reads do not repeat verifications (C2: 1431 of 1431 unique)
@@ -1222,13 +1226,17 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipEventRecord(e1, s));
       const OutSlots os = outSlots(b);
 #ifdef GWA_PROF
-      if (sf) throw std::runtime_error("the profiling build times -m bsf only");
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
-      launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
-                   scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount,
-                   ovfBits, rb, s, (uint32_t *)d_prof, -1);
+      if (sf)
+        launchSfSearch(b->R, qwFor(b->maxM), b->sfWrap, lanes, ix->view, b->scfg, b->st, rv,
+                       (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
+                       ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s, (uint32_t *)d_prof);
+      else
+        launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres,
+                     b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb,
+                     b->d_list[cur ^ 1], ovfCount, ovfBits, rb, s, (uint32_t *)d_prof, -1);
       {
         std::vector<uint64_t> pv((size_t)lanes * PR_N);
         HIPCHK(hipMemcpyAsync(pv.data(), d_prof, pv.size() * 8, hipMemcpyDeviceToHost, s));
@@ -1241,7 +1249,11 @@ int gwa_batch_run(gwa_batch_t *b) {
                                        "nStepLane", "dpFwd", "dpTrace", "sumWait", "nBuildWave", "nBuildLane",
                                        "wArenaGB", "eArena", "wWordGB", "eWord", "wDpGB", "eDp", "eDpWave",
                                        "wHitGB", "eHit", "wOutGB", "eOut", "-", "wave"};
-        fprintf(stderr, "[gwa-prof] tier %d reads %u lanes %u (Gcycles summed over waves; counts in M; bytes in GB):", t, n, lanes);
+        // -m sf (SfLane::sfStep): poll = queuePoll + state load, fm = rank2, nfa = the children's
+        // automaton steps, add1 = newState + offer, verify = addCandidate (dpFwd / dpTrace inside it),
+        // split = the candidate-set probe, seed = sfStart; nStep = polls, nVerify = DP verifications
+        fprintf(stderr, "[gwa-prof] %s", sf ? "-m sf " : "");
+        fprintf(stderr, "tier %d reads %u lanes %u (Gcycles summed over waves; counts in M; bytes in GB):", t, n, lanes);
         for (int q = 0; q < PR_N; ++q) {
           if (nm[q][0] == '-') continue;
           const bool count = (q >= PR_NVW && q <= PR_NSL) || q == PR_NWAIT || q == PR_NBW || q == PR_NBL ||

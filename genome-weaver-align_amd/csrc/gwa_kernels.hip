@@ -327,12 +327,12 @@ void launchSfSearch(int R, int QW, bool wrap, uint32_t lanes, const IndexView &i
                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                     const Caps &caps, OutHeader *oh, const OutSlots &os,
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
-                    hipStream_t s) {
+                    hipStream_t s, uint32_t *trace) {
   if (n == 0) return;
 #define GWA_L(Q, RR)                                                                                                   \
   if (QW == Q && R == RR) {                                                                                            \
     launchSfSearchQR<Q, RR>(wrap, lanes, ix, cfg, st, reads, list, n, scratch, laneStride, caps, oh, os, chrRank, work, \
-                            ovfList, ovfCount, ovfBits, s);                                                            \
+                            ovfList, ovfCount, ovfBits, s, trace);                                                            \
     return;                                                                                                            \
   }
 #define GWA_LQ(Q) GWA_L(Q, 4) GWA_L(Q, 8) GWA_L(Q, 16) GWA_L(Q, 32)

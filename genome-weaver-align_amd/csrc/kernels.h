@@ -23,7 +23,7 @@ void launchSfSearch(int R, int QW, bool wrap, uint32_t lanes, const IndexView &i
                     const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                     const Caps &caps, OutHeader *oh, const OutSlots &os,
                     const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
-                    hipStream_t s);
+                    hipStream_t s, uint32_t *trace = nullptr);
 void buildKmerTable(const IndexView &ix, int fm, int K, uint64_t *out, hipStream_t s);
 
 // batch_io.hip: reads in (encode on the device), SAM out (two-pass formatting), batch statistics

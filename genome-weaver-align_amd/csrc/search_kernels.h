@@ -104,7 +104,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
     for (uint32_t i = threadIdx.x; i < st.ldsCount; i += blockDim.x) stairLds[i] = st.tab[st.ldsBase + i];
     __syncthreads();
   }
-  typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8))> Lane;  // hybrid heap: k >= 4 with the LDS heap, sparse tiers
+  // hybrid heap: k >= 4 with the LDS heap, sparse tiers; the first tier's kernel (LH 1 without resume)
+  // keeps the DP slice (BsfLane DPM)
+  typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8)), 24, (LH == 1 && !RES) ? 1 : 0> Lane;
   Lane lane(ix, cfg, st, L, caps);
 #ifdef GWA_PROF
   lane.profG = prof;
@@ -217,11 +219,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 
 // sf_search<R, QW>: persistent lanes over the read list, one read per lane per iteration (lanes take
 // reads from a shared counter, one atomic per wavefront); overflowing reads go to the next tier.
-template <int R, int QW, bool WRAP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES)))
+// COOP (the sparse last tier, caps.sparse = 64): one read per wavefront, lane 0 searching and the
+// whole wavefront verifying -- lane 0 its due candidate, lanes 1-63 speculatively the candidates at
+// the top of its queue (SfLane::specJob); whole-column DP history (a lone traceback of tens of edits
+// would recompute a column per edit), one wave per SIMD (the few wavefronts need no occupancy).
+template <int R, int QW, bool WRAP, bool COOP>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? 1 : GWA_SEARCH_WAVES)))
 sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
                  uint8_t *scratch, uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
-                 const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits) {
+                 const int32_t *chrRank, uint32_t *work, uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits,
+                 uint32_t *trace) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t total = gridDim.x * blockDim.x;
   // scratch = [active lanes][laneStride] slices, then [lanes / 64][64-lane interleaved DP block]; a
@@ -236,8 +243,16 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
     __syncthreads();
   }
   __shared__ uint64_t qwLds[2 * QW * 256];
-  SfLane<R, QW, WRAP> lane(ix, cfg, st, L, caps);
+  SfLane<R, QW, WRAP, COOP ? 2 : 0> lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
+#ifdef GWA_PROF
+  // profiling build: the same [lanes][PR_N] slots as bsf_search_kernel (regions: SfLane::sfStep)
+  uint64_t *prof = (uint64_t *)trace + (size_t)gid * PR_N;
+  const uint64_t tk = clock64();
+  lane.profG = prof;
+#else
+  (void)trace;
+#endif
   if (st.ldsM >= 0) lane.stairLds = (lds_cu64 *)stairLds;
   lane.qwL = (lds_u64 *)(qwLds + threadIdx.x);
   lane.qwS = 256;
@@ -245,6 +260,79 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
   if (QW == 4) {
     lane.pmL = (lds_u64 *)(pmLds + threadIdx.x);
     lane.pmS = 256;
+  }
+  if constexpr (COOP) {
+    const int lid = (int)(gid & 63);
+    // a helper's CIGAR area: its share of the wavefront's (otherwise unused) path plane
+    const int hcap = caps.path / 2;
+    uint16_t *hcg = (uint16_t *)(chunk + L.oPath) + (size_t)lid * hcap;
+    for (;;) {
+      uint32_t i = 0;
+      if (lid == 0) i = atomicAdd(work, 1u);
+      i = __shfl(i, 0);
+      if (i >= n) break;
+      const uint32_t r = list[i];
+      const int m = (int)reads.len[r];
+      OutHeader *h = oh + r;
+      bool ovf = false;
+      if (m > 32 * QW) {
+        if (lid == 0) {
+          OutHeader z{};
+          z.status = ST_TOO_LONG;
+          *h = z;
+        }
+      } else {
+        lane.initRead(reads.codes + reads.off[r], m);
+        lane.coopClear(lid);
+        __threadfence_block();
+        int run = 0;
+        if (lid == 0) run = lane.sfBegin(false) ? 1 : 0;
+        else lane.buildMasks();  // (the helpers' DP reads the query words from their LDS rows)
+        for (;;) {
+          int need = 0;
+          if (lid == 0 && run) {
+            int stp = 1;
+            while (stp == 1) stp = lane.template sfStepT<true>();
+            need = stp == 2 ? 1 : 0;
+            run = need;
+          }
+          need = __shfl(need, 0);
+          if (!need) break;
+          const int hn = __shfl(lane.heapSize, 0), mm = __shfl(lane.minMismatches, 0), bs = __shfl(lane.bestScore, 0);
+          const bool job = lid == 0 || lane.specJob(lid, hn, mm, bs);
+          int rr = -1, pos = 0, diff = 0, co = 0, cl = 0;
+          if (job) {
+            if (lid != 0) {
+              lane.nCigar = 0;
+              lane.status = ST_UNMAPPED;
+            }
+            rr = lane.alignBlockDetailed(lane.jStrand, 0, m, lane.jRefStart, lane.jRefEnd, &pos, &diff, &co, &cl,
+                                         lid ? hcg : nullptr, lid ? hcap : 0);
+            if (lid != 0) lane.specPut(rr, pos, diff, co, cl, hcg);
+          }
+          __threadfence_block();
+          if (lid == 0) run = lane.candEnd(rr, pos, diff, co, cl) ? 1 : 0;
+        }
+        if (lid == 0) {
+          lane.writeSearchOutput(h, os, r);
+          h->states = lane.created;
+          h->quickSteps = lane.quickSteps;
+          h->blocks = 0;
+          h->kmerLookups = lane.kmerLookups;
+          h->quickShort = lane.shortSteps;
+          h->quickSa = 0;
+          h->quickText = 0;
+          ovf = h->status == ST_OVERFLOW;
+          if (ovf) atomicOr(ovfBits, (uint32_t)h->ovfWhat);
+        }
+      }
+      waveAppend(ovf, r, ovfList, ovfCount);
+    }
+#ifdef GWA_PROF
+    for (int q = 0; q < PR_N - 1; ++q) prof[q] += lane.prof[q];
+    if (__lane_id() == 0) prof[PR_N - 1] += clock64() - tk;
+#endif
+    return;
   }
   // the grown last tier (few reads, long searches): every caps.sparse-th lane only, so the searches
   // run on separate wavefronts instead of serialising inside one (bsf_search_kernel's sparse tiers)
@@ -282,6 +370,10 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
     }
     waveAppend(ovf, r, ovfList, ovfCount);
   }
+#ifdef GWA_PROF
+  for (int q = 0; q < PR_N - 1; ++q) prof[q] += lane.prof[q];
+  if (__lane_id() == 0) prof[PR_N - 1] += clock64() - tk;
+#endif
 }
 
 
@@ -306,7 +398,7 @@ void launchSearchQR(int ldsHeap, uint32_t lanes, const IndexView &ix, const Sear
   hipLaunchKernelGGL((bsf_search_kernel<R, QW, LL, RR>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
                      scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, res, trace, traceRead)
   if (ldsHeap == 2) GWA_CASE(2, true);
-  else if (ldsHeap && res.in) GWA_CASE(1, true);
+  else if (ldsHeap && (res.in || !caps.dpSlice)) GWA_CASE(1, true);  // (LH 1 without resume: the first tier only)
   else if (ldsHeap) GWA_CASE(1, false);
   else GWA_CASE(0, true);
 #undef GWA_CASE
@@ -318,14 +410,21 @@ template <int QW, int R>
 void launchSfSearchQR(bool wrap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                       const ReadsView &reads, const uint32_t *list, uint32_t n, uint8_t *scratch, uint64_t laneStride,
                       const Caps &caps, OutHeader *oh, const OutSlots &os, const int32_t *chrRank, uint32_t *work,
-                      uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s) {
+                      uint32_t *ovfList, uint32_t *ovfCount, uint32_t *ovfBits, hipStream_t s, uint32_t *trace) {
   dim3 grid((lanes + 255) / 256);
-  if (wrap || QW == 16)
-    hipLaunchKernelGGL((sf_search_kernel<R, QW, true>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,
-                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);
-  else if (QW != 16)
-    hipLaunchKernelGGL((sf_search_kernel<R, QW, QW == 16>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,
-                       laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits);
+  // the cooperative kernel for the sparse last tier (one read per wavefront, caps.spec > 0)
+  const bool coop = caps.sparse == 64 && caps.spec > 0;
+#define GWA_SF(WW, CC)                                                                                                 \
+  hipLaunchKernelGGL((sf_search_kernel<R, QW, WW, CC>), grid, dim3(256), 0, s, ix, cfg, st, reads, list, n, scratch,  \
+                     laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, trace)
+  if (wrap || QW == 16) {
+    if (coop) GWA_SF(true, true);
+    else GWA_SF(true, false);
+  } else if (QW != 16) {
+    if (coop) GWA_SF(QW == 16, true);
+    else GWA_SF(QW == 16, false);
+  }
+#undef GWA_SF
 }
 
 // explicit instantiation (search_inst.hip: `template`) or declaration (`extern template`) of one
@@ -339,7 +438,7 @@ void launchSfSearchQR(bool wrap, uint32_t lanes, const IndexView &ix, const Sear
   KW void launchSfSearchQR<QW_, R_>(bool, uint32_t, const IndexView &, const SearchConfig &, const StairTables &,  \
                                     const ReadsView &, const uint32_t *, uint32_t, uint8_t *, uint64_t,           \
                                     const Caps &, OutHeader *, const OutSlots &, const int32_t *, uint32_t *,      \
-                                    uint32_t *, uint32_t *, uint32_t *, hipStream_t);
+                                    uint32_t *, uint32_t *, uint32_t *, hipStream_t, uint32_t *);
 #define GWA_SEARCH_EXTERN_QW(QW_)                                                                                  \
   GWA_SEARCH_INSTANCE(extern template, QW_, 4)                                                                    \
   GWA_SEARCH_INSTANCE(extern template, QW_, 8)                                                                    \

@@ -53,9 +53,10 @@ GWA_HD bool sfChunksWrap(int m_, int kk) {
 
 // WRAP: the batch has reads whose chunk starts wrap (sfChunksWrap); without them the automaton's
 // out-of-table mask path is compiled out (it cost the R = 8 kernel ~35 spilled VGPRs)
-template <int R, int QW, bool WRAP = true>
-struct SfLane : BsfLane<R, QW, false, 24> {
-  typedef BsfLane<R, QW, false, 24> B;
+// DPM: the DP history mode (BsfLane); the cooperative sparse kernel keeps whole columns (2)
+template <int R, int QW, bool WRAP = true, int DPM = 0>
+struct SfLane : BsfLane<R, QW, false, 24, DPM> {
+  typedef BsfLane<R, QW, false, 24, DPM> B;
   using B::ix;
   using B::cfg;
   using B::L;
@@ -74,6 +75,14 @@ struct SfLane : BsfLane<R, QW, false, 24> {
   using B::saReads;
   using B::kmerLookups;
   using B::shortSteps;
+  using B::nCigar;
+  using B::numSW;
+  using B::verifyBytes;
+  using B::ovfWhat;
+#ifdef GWA_PROF
+  using B::prof;
+  using B::profG;
+#endif
 
   GWA_HD SfLane(const IndexView &ix_, const SearchConfig &c_, const StairTables &s_, LaneMem<R> L_, Caps caps_)
       : B(ix_, c_, s_, L_, caps_) {}
@@ -110,11 +119,11 @@ struct SfLane : BsfLane<R, QW, false, 24> {
   }
 
   // candidates[strand].contains(start) / add: a linear scan of L.cand() for the small sets of the
-  // first tiers; an open-addressing hash table (caps.cand slots, a power of two, at most half full)
-  // when caps.cand >= kCandHash -- the deep tiers hold reads with tens of thousands of candidates,
-  // where a scan per candidate would be quadratic.  Only membership is used (:304-306), so the
-  // table's order does not matter.
-  static constexpr int kCandHash = 4096;
+  // first tier; an open-addressing hash table (caps.cand slots, a power of two, at most half full)
+  // when caps.cand >= kCandHash -- the deeper tiers hold reads with up to hundreds of thousands of
+  // candidates, where a scan per candidate (one dependent load per entry) would be quadratic.  Only
+  // membership is used (:304-306), so the table's order does not matter.
+  static constexpr int kCandHash = 64;
   static constexpr int64_t kCandEmpty = (int64_t)0x8000000000000000LL;
   GWA_HD void candClear() {
     nCand = 0;
@@ -143,6 +152,26 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     c[h] = key;
     ++nCand;
     return 1;
+  }
+
+  // candidates[strand].contains(start), without adding it (the helper lanes of the cooperative kernel)
+  GWA_HD bool candHas(int64_t key) const {
+    const int64_t *c = L.cand();
+    if (caps.cand < kCandHash) {
+      int hit = 0;
+      for (int i = 0; i < nCand; ++i) hit |= c[i] == key ? 1 : 0;
+      return hit != 0;
+    }
+    const uint32_t mask = (uint32_t)caps.cand - 1u;
+    uint32_t h = (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ULL) >> 40) & mask;
+    int found = 0, go = 1;
+    for (int q = 0; go && q < caps.cand; ++q) {
+      const int64_t v = c[h];
+      found = v == key ? 1 : 0;
+      go = (found == 0 && v != kCandEmpty) ? 1 : 0;
+      h = (h + 1u) & mask;
+    }
+    return found != 0;
   }
 
   // SFState.compareTo (:463-469) as a heap key: kOffset ascending, then score descending
@@ -272,15 +301,20 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     return true;
   }
 
-  // AlignmentResultHolder.add (:369-389) for a single-hit chain (no splits on this path)
+  // AlignmentResultHolder.add (:369-389) for a single-hit chain (no splits on this path).  After
+  // every add each listed hit has diff <= minMismatches (reportResult drops the others, :349-350),
+  // so the rebuild of the list (:381-388) can only drop entries when this add lowers minMismatches:
+  // only then is the list scanned (at most k + 1 times per read; reads on repeats list thousands of
+  // hits, and a scan per add was quadratic in them)
   GWA_HD void sfResultAdd(int hit, int diff) {
-    if (m > 0 && diff < minMismatches) {
+    const bool lower = m > 0 && diff < minMismatches;
+    if (lower) {
       minMismatches = diff;
       bestScore = m * cfg.matchScore - diff * cfg.mismatchPenalty;
     }
     if (maxMatchLength < m) maxMatchLength = m;
-    int n = 0;
-    for (int i = 0; i < listSize; ++i) {
+    int n = lower ? 0 : listSize;
+    for (int i = 0; lower && i < listSize; ++i) {
       const int e = L.list()[i];
       if (L.hits()[e].diff <= minMismatches) L.list()[n++] = e;
     }
@@ -293,56 +327,201 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     listSize = n;
   }
 
-  // addCandidate (:298-343); false = the search ends (overflow / error)
-  GWA_HD bool addCandidate(const SfState<R> &c) {
-    if (c.ub - c.lb != 1) return true;  // multi hit: nothing (:339-342)
-    const int strand = c.strand;
-    // toCoordinate(si.lowerBound, strand, Forward) (A/FMIndexOnGenome.java:227-238), full SA
+  // The verification job of a candidate: alignBlockDetailed(jStrand, 0, m, jRefStart, jRefEnd), a pure
+  // function of (start, strand) = jKey
+  int jStrand = 0;
+  int64_t jRefStart = 0, jRefEnd = 0, jKey = 0;
+  // toCoordinate(si.lowerBound, strand, Forward) (A/FMIndexOnGenome.java:227-238) of a single-row
+  // state, as the candidate's start position (:301-303) and its set key start << 1 | strand
+  GWA_HD int64_t candStart(uint32_t lb, int strand, int index, uint8_t meta, int64_t *key) {
     const int fm = strand == 0 ? 1 : 0;
     int64_t v;
-    if (c.meta & M_TEXT) {
-      v = (int64_t)c.lb;
+    if (meta & M_TEXT) {
+      v = (int64_t)lb;
     } else {
-      v = (int64_t)ix.sa[fm][c.lb];
+      v = (int64_t)ix.sa[fm][lb];
       ++saReads;
     }
     const int64_t seqIndex = fm == 0 ? v : (int64_t)ix.N - v;
-    const int offsetFromSearchHead = strand == 0 ? c.index : m - c.index;
+    const int offsetFromSearchHead = strand == 0 ? index : m - index;
     const int64_t start = seqIndex - offsetFromSearchHead;
-    const int64_t key = (int64_t)((uint64_t)start << 1) | strand;
+    *key = (int64_t)((uint64_t)start << 1) | strand;
+    return start;
+  }
+  // addCandidate (:298-343) up to the verification: 0 = done (*go: false = the search ends, overflow /
+  // error), 1 = the job (jStrand, jRefStart, jRefEnd) is to be verified, then candEnd
+  GWA_HD int candBegin(const SfState<R> &c, bool *go) {
+    *go = true;
+    if (c.ub - c.lb != 1) return 0;  // multi hit: nothing (:339-342)
+    int64_t key;
+    const int64_t start = candStart(c.lb, c.strand, c.index, c.meta, &key);
+    GWA_PT(tci);
     const int ins = candInsert(key);
-    if (ins == 0) return true;  // candidates[strand].contains(start)
+    GWA_PA(PR_SPLIT, tci);
+    if (ins == 0) return 0;  // candidates[strand].contains(start)
     if (ins < 0) {
       B::ovf(OV_CAND);
-      return false;
+      *go = false;
+      return 0;
     }
     const int64_t refStart = start - k > 0 ? start - k : 0;
     const int64_t refEnd = start + m + k < (int64_t)ix.N ? start + m + k : (int64_t)ix.N;
     if (refStart > refEnd) {  // ACGTSequence.subString throws
       status = ST_ERROR;
-      return false;
+      *go = false;
+      return 0;
     }
-    int pos = 0, diff = 0, co = 0, cl = 0;
-    // the whole read, reversed on strand 1 (:317-321)
-    const int r = B::alignBlockDetailed(strand, 0, m, refStart, refEnd, &pos, &diff, &co, &cl);
+    jStrand = c.strand;  // the whole read, reversed on strand 1 (:317-321)
+    jRefStart = refStart;
+    jRefEnd = refEnd;
+    jKey = key;
+    return 1;
+  }
+  // addCandidate after the verification r (0 alignment, 1 null, < 0 overflow); false = the search ends
+  GWA_HD bool candEnd(int r, int pos, int diff, int co, int cl) {
     if (r < 0) return false;
     if (r == 1) return true;  // alignment == null
     // a dropped hit's CIGAR ops are released (the lane's CIGAR area then holds the listed hits' ops
     // only: reads on repeats verify millions of candidates)
     int32_t chr, p;
-    if (B::translate(refStart + pos + 1, &chr, &p) != 0) {  // UTGBException is logged
-      B::nCigar = co;
+    if (B::translate(jRefStart + pos + 1, &chr, &p) != 0) {  // UTGBException is logged
+      nCigar = co;
       return true;
     }
     // reportResult (:345-353): total match length m; a hit above minMismatches is dropped
     if (m == 0 || diff > minMismatches) {
-      B::nCigar = co;
+      nCigar = co;
       return true;
     }
-    const int h = B::newHit(chr, p, m, 0, m, diff, strand, co, cl, 1);
+    const int h = B::newHit(chr, p, m, 0, m, diff, jStrand, co, cl, 1);
     if (h < 0) return false;
     sfResultAdd(h, diff);
     return status != ST_OVERFLOW;
+  }
+  GWA_HD bool addCandidate(const SfState<R> &c) {
+    bool go;
+    if (!candBegin(c, &go)) return go;
+    int pos = 0, diff = 0, co = 0, cl = 0;
+    GWA_PC(PR_NVW, PR_NVL);
+    const int r = B::alignBlockDetailed(jStrand, 0, m, jRefStart, jRefEnd, &pos, &diff, &co, &cl);
+    return candEnd(r, pos, diff, co, cl);
+  }
+
+  // ---- speculative verification (the cooperative kernel of the sparse last tier) ----
+  // Lane 0 of a wavefront runs the read's search; when a verification is due whose result is not in
+  // the speculation table, the whole wavefront runs DPs: lane 0 its own, lanes 1-63 those of the
+  // single-row states at queue entries 1-63 -- the next polls, mostly -- that the owner would verify
+  // when polled (the cutoff thresholds only tighten, so a state cut now is cut then) and whose start
+  // is neither verified nor speculated yet.  A result is a pure function of the job, so taking it
+  // from the table when the owner reaches the candidate changes nothing but the time.  Table entry:
+  // the key, the result and a CIGAR of up to 20 ops (longer ones are not kept); open addressing with
+  // at most kSpecProbe probes, slots claimed by compare-and-swap.
+  struct SpecEntry {
+    int64_t key;
+    int32_t r, diff, pos;
+    uint16_t ncig, pad;
+    uint16_t ops[20];
+  };
+  static constexpr int kSpecOps = 20, kSpecProbe = 32;
+  GWA_HD SpecEntry *spec() const { return (SpecEntry *)(L.slice + L.oSpec); }
+  GWA_HD uint32_t specSlot(int64_t key) const {
+    return (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ULL) >> 40) & ((uint32_t)caps.spec - 1u);
+  }
+  // the owner: the result of job jKey from the table, with alignBlockDetailed's effects (counters,
+  // CIGAR appended); false = not there
+  GWA_HD bool specTake(int *r, int *pos, int *diff, int *co, int *cl) {
+    uint32_t h = specSlot(jKey);
+    int at = -1, go = 1;
+    for (int q = 0; go && q < kSpecProbe; ++q) {
+      const int64_t v = spec()[h].key;
+      at = v == jKey ? (int)h : -1;
+      go = (at < 0 && v != kCandEmpty) ? 1 : 0;
+      h = (h + 1u) & ((uint32_t)caps.spec - 1u);
+    }
+    if (at < 0) return false;
+    const SpecEntry &e = spec()[at];
+    const int N = (int)(jRefEnd - jRefStart), bMax = (m + 63) / 64 > 0 ? (m + 63) / 64 : 1;
+    ++numSW;
+    verifyBytes += (2 * N + 7) / 8 + (N + 7) / 8 + 32 * bMax;
+    *r = e.r;
+    if (e.r != 0) return true;
+    const int n = e.ncig;
+    if (nCigar + n + 4 > caps.cigar) {
+      B::ovf(OV_CIGAR);
+      *r = -1;
+      return true;
+    }
+    for (int i = 0; i < n; ++i) L.cigar()[nCigar + i] = e.ops[i];
+    *co = nCigar;
+    *cl = n;
+    nCigar += n;
+    *pos = e.pos;
+    *diff = e.diff;
+    return true;
+  }
+  // a helper lane (lane j of the owner's wavefront, sharing its slice): its job from queue entry j of
+  // the owner's queue of hn entries at thresholds mm / bs; false = none
+  GWA_HD bool specJob(int j, int hn, int mm, int bs) {
+    if (j >= hn) return false;
+    const int idx = (int)(L.heapP[j] & ((1ULL << 24) - 1ULL));  // (KS = 24; the slice heap, hs = 1)
+    const SfState<R> *p = arena() + idx;
+    const uint32_t lb = p->lb, ub = p->ub;
+    const int score = p->score, offset = p->offset, index = p->index;
+    const int strand = p->strand, kOffset = p->kOffset;
+    const uint8_t meta = p->meta;
+    const int ubScore = score + (offset + (m - index)) * cfg.matchScore;
+    if (kOffset > mm || ubScore < bs || ub - lb != 1) return false;
+    int64_t key;
+    const int64_t start = candStart(lb, strand, index, meta, &key);
+    const int64_t refStart = start - k > 0 ? start - k : 0;
+    const int64_t refEnd = start + m + k < (int64_t)ix.N ? start + m + k : (int64_t)ix.N;
+    if (refStart > refEnd || candHas(key)) return false;
+    uint32_t h = specSlot(key);
+    int go = 1, seen = 0;
+    for (int q = 0; go && q < kSpecProbe; ++q) {
+      const int64_t v = spec()[h].key;
+      seen = v == key ? 1 : 0;
+      go = (seen == 0 && v != kCandEmpty) ? 1 : 0;
+      h = (h + 1u) & ((uint32_t)caps.spec - 1u);
+    }
+    if (seen) return false;
+    jStrand = strand;
+    jRefStart = refStart;
+    jRefEnd = refEnd;
+    jKey = key;
+    return true;
+  }
+  // a helper lane: keep its result (r >= 0; a CIGAR of <= kSpecOps ops, from its own area cg)
+  GWA_HD void specPut(int r, int pos, int diff, int co, int cl, const uint16_t *cg) {
+    if (r < 0 || (r == 0 && cl > kSpecOps)) return;
+    uint32_t h = specSlot(jKey);
+    int at = -1, go = 1;
+    for (int q = 0; go && q < kSpecProbe; ++q) {
+#ifdef __HIP_DEVICE_COMPILE__
+      const unsigned long long old = atomicCAS((unsigned long long *)&spec()[h].key, (unsigned long long)kCandEmpty,
+                                               (unsigned long long)jKey);
+#else
+      const unsigned long long old = (unsigned long long)spec()[h].key;
+      if (old == (unsigned long long)kCandEmpty) spec()[h].key = jKey;
+#endif
+      at = old == (unsigned long long)kCandEmpty ? (int)h : -1;
+      go = (at < 0 && old != (unsigned long long)jKey) ? 1 : 0;  // (another lane holds this key: done)
+      h = (h + 1u) & ((uint32_t)caps.spec - 1u);
+    }
+    if (at < 0) return;
+    SpecEntry &e = spec()[at];
+    e.r = r;
+    e.diff = diff;
+    e.pos = pos;
+    e.ncig = (uint16_t)(r == 0 ? cl : 0);
+    for (int i = 0; r == 0 && i < cl; ++i) e.ops[i] = cg[co + i];
+  }
+  // the candidate set and the speculation table emptied by the 64 lanes of the wavefront together
+  GWA_HD void coopClear(int lid) {
+    nCand = 0;
+    if (caps.cand >= kCandHash)
+      for (int i = lid; i < caps.cand; i += 64) L.cand()[i] = kCandEmpty;
+    for (int i = lid; i < caps.spec; i += 64) spec()[i].key = kCandEmpty;
   }
 
   // SFState.nextState (:448-460) + ReadAlignmentNFA.nextState(nextACGTIndex, progress, m, ...)
@@ -351,47 +530,83 @@ struct SfLane : BsfLane<R, QW, false, 24> {
     if (!B::stairOk()) return false;  // c.nextState(..., getStairCaseFilter(m)) (:282)
     const int nextIndex = c.index + 1;
     const int kr = c.nrows - 1;
+    GWA_PT(tq);
     const int64_t qeq = B::patternMask64(c.strand, true, nextIndex, 0, nextIndex, ch, kr);
     uint64_t rows[R];
     int nh = 0, nko = 0;
     bool hm = false;
     if (!B::template nfaCore<WRAP>(c.nfa, c.nrows, c.kOffset, qeq, nextIndex - c.offset, m - c.offset, rows, &nh, &nko, &hm))
       return true;  // null: numFiltered++
+    GWA_PA(PR_NFA, tq);
+    GWA_PT(ta);
     const int diff = nko - c.kOffset;
     int newScore = c.score - diff * cfg.mismatchPenalty;
     if (diff == 0) newScore++;
     const int id = newState(c.strand, c.offset, nextIndex, newScore, lb, ub, 0, rows, nh, nko, hm);
     if (id < 0) return false;
     push(id, nko, newScore);
+    GWA_PA(PR_ADD1, ta);
     return status != ST_OVERFLOW;
   }
 
-  // one iteration of the queue loop (:257-290); false = the loop ended
-  GWA_HD bool sfStep() {
-    if (heapSize == 0 || status == ST_OVERFLOW || status == ST_ERROR) return false;
+  // one iteration of the queue loop (:257-290): 0 = the loop ended, 1 = go on; COOP (the owner lane
+  // of the cooperative kernel): 2 = a verification is due (jStrand, jRefStart, jRefEnd) that the
+  // speculation table does not hold -- the wavefront runs it, then candEnd
+  template <bool COOP>
+  GWA_HD int sfStepT() {
+    if (heapSize == 0 || status == ST_OVERFLOW || status == ST_ERROR) return 0;
+    GWA_PT(tp);
     const int idx = B::queuePoll();
     const SfState<R> c = arena()[idx];
     sfFree(idx);
+    GWA_PC(PR_NSW, PR_NSL);
+    GWA_PA(PR_POLL, tp);
     const int ubScore = c.score + (c.offset + (m - c.index)) * cfg.matchScore;  // scoreUpperBound (:444-446)
-    if ((int)c.kOffset > minMismatches || ubScore < bestScore) return true;    // numCutOff++
-    if (c.hasHit || c.index >= m || c.ub - c.lb == 1) return addCandidate(c);
+    if ((int)c.kOffset > minMismatches || ubScore < bestScore) return 1;    // numCutOff++
+    if (c.hasHit || c.index >= m || c.ub - c.lb == 1) {
+      GWA_PT(tv);
+      int res;
+      if (COOP) {
+        bool go;
+        if (!candBegin(c, &go)) {
+          res = go ? 1 : 0;
+        } else {
+          int r = 0, pos = 0, diff = 0, co = 0, cl = 0;
+          res = specTake(&r, &pos, &diff, &co, &cl) ? (candEnd(r, pos, diff, co, cl) ? 1 : 0) : 2;
+        }
+      } else {
+        res = addCandidate(c) ? 1 : 0;
+      }
+      GWA_PA(PR_VERIFY, tv);
+      return res;
+    }
     // fmIndex.forwardSearch(strand, si) (A/FMIndexOnGenome.java:203-225): the four base extensions
     const int fm = c.strand == 0 ? 1 : 0;
     uint64_t lo[5], hi[5];
+    GWA_PT(tf);
     B::rank2(fm, c.lb, c.ub, lo, hi);
+    GWA_PA(PR_FM, tf);
     ++numFMIndexSearches;
     for (int ch = 0; ch < 4; ++ch) {  // ACGT.exceptN
       const uint64_t l = ix.C[ch] + lo[ch], u = ix.C[ch] + hi[ch];
-      if (l < u && !child(c, ch, (uint32_t)l, (uint32_t)u)) return false;
+      if (l < u && !child(c, ch, (uint32_t)l, (uint32_t)u)) return 0;
     }
-    return true;
+    return 1;
   }
+  GWA_HD bool sfStep() { return sfStepT<false>() != 0; }
 
-  GWA_HD void sfSearch() {
-    candClear();
+  // align_internal's start (candidate set emptied by the caller in the cooperative kernel)
+  GWA_HD bool sfBegin(bool clear) {
+    if (clear) candClear();
     freeHead = spare = -1;
     created = 0;
-    if (!sfStart()) return;
+    GWA_PT(tsd);
+    const bool go = sfStart();
+    GWA_PA(PR_SEED, tsd);
+    return go;
+  }
+  GWA_HD void sfSearch() {
+    if (!sfBegin(true)) return;
     while (sfStep()) {
     }
   }

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <algorithm>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../genome-weaver-align_amd/csrc/bsf_core.h"
@@ -24,6 +25,7 @@ struct HC {
 };
 
 static uint64_t g_suspends = 0;  // reads suspended (and resumed on the next tier), all calls
+static uint64_t g_specJobs = 0, g_specMiss = 0, g_specTaken = 0;  // HC_SF_COOP: helper verifications, the owner's own, taken from the table
 
 // the GPU's capacity tiers (gwa_api.cpp kTiers) replayed on the CPU
 template <int R, int QW>
@@ -42,8 +44,8 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
                          {1024, 1024, w ? 256 : 64, w ? 256 : 64, w ? 4096 : 1024, dpw, path, 0, 0},
                          {4096, 4096, 256, 256, 4096, dpw, path, 0, 0}, {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 0}};
   // -m sf tiers (gwa_api.cpp kSfTiers)
-  const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, sl, 32, 0, 1}, {2048, 2048, 64, 64, 2048, dpw, path, 0, 256, 0, 1},
-                           {8192, 8192, 256, 256, 4096, dpw, path, 0, 1024, 0, 1},
+  const Caps sfTiers[4] = {{512, 512, 32, 32, 512, dpw, path, sl, 32, 0, 1}, {2048, 2048, 64, 64, 2048, dpw, path, 0, 512, 0, 1},
+                           {8192, 8192, 256, 256, 4096, dpw, path, 0, 2048, 0, 1},
                            {65536, 65536, 4096, 4096, 65536, dpw, path, 0, 16384, 0, 1}};
   std::vector<uint8_t> scratch(std::max(laneBytes<R>(tiers[3]), laneBytes<R>(sfTiers[3])) + ilvBytes(tiers[3]) + 4096);
   // one read at a time: a one-slot OutSlots whose pool is large enough for any report
@@ -87,9 +89,71 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         bc.cand = 64;
         while (bc.cand < 2 * bc.hits && bc.cand < (1 << 22)) bc.cand <<= 1;
       }
+      // HC_SF_COOP=1: -m sf through the cooperative kernel's algorithm (search_kernels.h sf_search_kernel
+      // COOP: speculative verification by 63 helper lanes sharing the slice) on every tier
+      const bool coop = strategy == 1 && getenv("HC_SF_COOP") && atoi(getenv("HC_SF_COOP")) != 0;
+      if (coop) {
+        sc.spec = 64;
+        while (sc.spec < sc.cand) sc.spec <<= 1;
+      }
       {
         const size_t need = std::max(laneBytes<R>(sc), laneBytes<R>(bc)) + ilvBytes(bc) + 4096;
         if (scratch.size() < need) scratch.resize(need);
+      }
+      if (coop) {
+        typedef SfLane<R, QW, true, 2> CL;
+        LaneMem<R> L = laneMem<R>(scratch.data(), sc);
+        const int hcap = sc.path / 2;
+        static std::vector<uint8_t> hchunk;
+        static std::vector<uint16_t> hcig;
+        hchunk.assign((size_t)64 * (ilvBytes(sc) + 64), 0);
+        hcig.assign((size_t)64 * hcap, 0);
+        std::vector<CL> ln;
+        ln.reserve(64);
+        for (int h = 0; h < 64; ++h) {
+          LaneMem<R> Lh = laneMem<R>(scratch.data(), hchunk.data() + (size_t)h * (ilvBytes(sc) + 64), 0, 1, sc);
+          ln.emplace_back(x->v, cfg, st, h == 0 ? L : Lh, sc);
+          ln[h].chrRank = rk.data();
+          ln[h].initRead(codes.data(), (int)mlen);
+        }
+        for (int h = 0; h < 64; ++h) ln[h].coopClear(h);
+        for (int h = 1; h < 64; ++h) ln[h].buildMasks();
+        CL &o = ln[0];
+        hd = OutHeader{};
+        int run = o.sfBegin(false) ? 1 : 0;
+        int miss = 0;
+        for (;;) {
+          int need = 0;
+          if (run) {
+            int stp = 1;
+            while (stp == 1) stp = o.template sfStepT<true>();
+            need = stp == 2 ? 1 : 0;
+            run = need;
+          }
+          if (!need) break;
+          for (int h = 1; h < 64; ++h) {
+            if (!ln[h].specJob(h, o.heapSize, o.minMismatches, o.bestScore)) continue;
+            int pos = 0, diff = 0, co = 0, cl = 0;
+            ln[h].nCigar = 0;
+            ln[h].status = ST_UNMAPPED;
+            uint16_t *cg = hcig.data() + (size_t)h * hcap;
+            const int r = ln[h].alignBlockDetailed(ln[h].jStrand, 0, (int)mlen, ln[h].jRefStart, ln[h].jRefEnd, &pos, &diff, &co,
+                                                   &cl, cg, hcap);
+            ln[h].specPut(r, pos, diff, co, cl, cg);
+            ++g_specJobs;
+          }
+          int pos = 0, diff = 0, co = 0, cl = 0;
+          const int r = o.alignBlockDetailed(o.jStrand, 0, (int)mlen, o.jRefStart, o.jRefEnd, &pos, &diff, &co, &cl);
+          ++g_specMiss;
+          ++miss;
+          run = o.candEnd(r, pos, diff, co, cl) ? 1 : 0;
+        }
+        g_specTaken += (uint64_t)(o.numSW - miss);
+        used[0] = used[1] = used[2] = 0;
+        o.writeSearchOutput(&hd, os, 0);
+        hd.quickSteps = o.quickSteps;
+        if (hd.status != ST_OVERFLOW) break;
+        continue;
       }
       if (strategy == 1) {
         LaneMem<R> L = laneMem<R>(scratch.data(), sc);
@@ -104,9 +168,11 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         if (hd.status != ST_OVERFLOW) break;
         continue;
       }
+      // the first tier's kernel keeps the DP slice (BsfLane DPM 1, search_kernels.h), the others checkpoints
+      auto tier = [&](auto dpm) -> bool {  // false: the read is done
+      typedef BsfLane<R, QW, false, 24, decltype(dpm)::value> Lane;
       LaneMem<R> L = laneMem<R>(scratch.data(), bc);
-      BsfLane<R, QW> lane(x->v, cfg, st, L, bc);
-      typedef BsfLane<R, QW> Lane;
+      Lane lane(x->v, cfg, st, L, bc);
       lane.chrRank = rk.data();
       const char *tre = getenv("GWA_TRACE_READ");
       const char *qtre = getenv("GWA_QTRACE_READ");
@@ -129,7 +195,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
       haveRec = false;
       if (phase == -1) {  // the quick scan finished the read
         if (traced) tv[0] = (uint32_t)lane.traceN;
-        break;
+        return false;
       }
       while (phase == Lane::LP_RUN || phase == Lane::LP_WAIT) phase = phase == Lane::LP_RUN ? lane.laneStep() : lane.laneReport();
       if (phase == Lane::LP_SUSPEND) {
@@ -146,7 +212,10 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
       }
       if (traced) tv[0] = (uint32_t)lane.traceN;
       if (hd.status == ST_OVERFLOW && getenv("HC_OVF_LOG")) fprintf(stderr, "[hc] read %u tier %d overflow 0x%x\n", i, t, hd.ovfWhat);
-      if (hd.status != ST_OVERFLOW) break;
+      return hd.status == ST_OVERFLOW;
+      };
+      const bool more = t == 0 ? tier(std::integral_constant<int, 1>()) : tier(std::integral_constant<int, 0>());
+      if (!more) break;
     }
     if (traced) {
       FILE *tf = fopen("hc_trace.bin", "wb");
@@ -219,6 +288,7 @@ void *hc_index_fasta(const char *text, uint64_t len) {
 void hc_index_free(void *p) { delete (HC *)p; }
 
 uint64_t hc_suspends(void) { return g_suspends; }
+void hc_spec_stats(uint64_t *out) { out[0] = g_specJobs; out[1] = g_specMiss; out[2] = g_specTaken; }
 
 int hc_sa(void *p, int strand, uint32_t *out) {
   auto *x = (HC *)p;

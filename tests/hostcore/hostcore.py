@@ -24,6 +24,7 @@ def lib():
         L.hc_index_fasta.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
         L.hc_index_free.argtypes = [ctypes.c_void_p]
         L.hc_suspends.restype = ctypes.c_uint64
+        L.hc_spec_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
         L.hc_sa.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.hc_align.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                ctypes.c_void_p,
@@ -75,3 +76,11 @@ class HostCore:
 def suspends():
     """reads the host replay of the tiers has suspended and resumed so far (all calls)"""
     return lib().hc_suspends()
+
+
+def spec_stats():
+    """HC_SF_COOP runs so far: (helper-lane speculative verifications, verifications the owner ran
+    itself, verifications the owner took from the speculation table)"""
+    v = (ctypes.c_uint64 * 3)()
+    lib().hc_spec_stats(v)
+    return int(v[0]), int(v[1]), int(v[2])

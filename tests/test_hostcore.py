@@ -144,6 +144,28 @@ def test_sf_repetitive_genome(repetitive_genome, m, k, sub, chim):
     _cmp(codes, names, lengths, _mk(codes, 120, m, sub, chim, seed=m * 11 + int(chim)), k, strategy=1)
 
 
+@pytest.mark.parametrize("case", ["indels150", "rep100", "rep50chim", "rep_rt2"])
+def test_sf_cooperative_speculation(random_genome, repetitive_genome, case, monkeypatch):
+    """-m sf through the cooperative kernel's algorithm (search_kernels.h sf_search_kernel COOP, run
+    by the GPU on the sparse last tier), here on every tier: 63 helper lanes verify the candidates at
+    the top of the owner's queue ahead of time and the owner takes those results from the table.
+    The SAM must equal the oracle's, and most verifications must come from the helpers."""
+    monkeypatch.setenv("HC_SF_COOP", "1")
+    j0, m0, t0 = hostcore.spec_stats()
+    if case == "indels150":
+        codes, names, lengths = random_genome
+        seqs, rn = synth.reads(codes, lengths, 150, 150, config_id=24, indels=True, max_edits=5)
+        strs = synth.to_strings(seqs)
+        _cmp(codes, names, lengths, [(rn[i], strs[i], None) for i in range(len(strs))], 5.0, strategy=1)
+    else:
+        codes, names, lengths = repetitive_genome
+        m, sub, chim, rt = {"rep100": (100, 2, False, 0), "rep50chim": (50, 3, True, 0), "rep_rt2": (100, 2, False, 2)}[case]
+        _cmp(codes, names, lengths, _mk(codes, 120, m, sub, chim, seed=m * 13 + int(chim)), 2.0, rt=rt, strategy=1)
+    j1, m1, t1 = hostcore.spec_stats()
+    print("speculative verifications %d, owner's own %d, taken %d" % (j1 - j0, m1 - m0, t1 - t0))
+    assert j1 - j0 > 0 and m1 - m0 > 0 and t1 - t0 > 0
+
+
 @pytest.mark.parametrize("rt", [1, 2])
 def test_sf_report_modes(repetitive_genome, rt):
     codes, names, lengths = repetitive_genome

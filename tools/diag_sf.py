@@ -5,6 +5,8 @@ time limit, to show how far the reference algorithm gets on them; then the oracl
 that needed a tier >= 1 when the batch finished, SAM compared.
 
   python tools/diag_sf.py [reads] [strategy] [oracle reads] [state cap]
+
+(oracle reads 0: the GPU batch only.)
 """
 import multiprocessing as mp
 import os
@@ -82,6 +84,9 @@ def main():
         got, _ = b.results_select(deep.astype(np.uint32))
     heavy = [int(i) for i in np.argsort(-c[:, 12], kind="stable")[:n_orc]]
     b.close()
+    if n_orc == 0:  # GPU side only (e.g. GWA_LIB=libgwa_prof.so: per-region cycles per tier)
+        gi.close()
+        return
     import oracle as O
     t0 = time.time()
     sa_f = gi.suffixArray(0)
