@@ -268,7 +268,8 @@ GWA_HD size_t laneBytes(const Caps &c) {  // per-lane slice
   b += sizeof(DHit) * (size_t)c.hits;
   b += 4 * (size_t)c.list;
   b += 2 * (size_t)c.cigar;
-  if (c.spec > 0) b = ((b + 63) & ~(size_t)63) + 64 * (size_t)c.spec;
+  // (-m sf cooperative kernel: result table, deferred jobs, undo log; SfLane)
+  if (c.spec > 0) b = ((b + 63) & ~(size_t)63) + 64 * (size_t)c.spec + 32 * (size_t)kSfDJobs + 16 * (size_t)kSfULog;
   return (b + 255) & ~(size_t)255;
 }
 GWA_HD size_t ilvBytes(const Caps &c) {  // interleaved bytes per lane
@@ -904,6 +905,19 @@ struct BsfLane {
   // Heap slot i: the LDS / slice array of the kernel instance (first tier: LDS), or, with the hybrid
   // heap (HY; k >= 4 kernels: their heaps outgrow a small LDS array, deep heaps are rare), LDS for the
   // top slots and the slice beyond them -- one flat address either way
+  // Undo log of the queue's writes (DPM 2: the cooperative -m sf kernel's deferred verification,
+  // SfLane): while uOn, every queue slot written is logged first as (slot, old entry), so the
+  // queue can be put back as it was when the deferral began
+  uint64_t *ulogP = nullptr;
+  int uN = 0, uOn = 0;
+  GWA_HD void ulogPut(uint64_t tag, uint64_t old) {
+    ulogP[2 * (size_t)uN] = tag;
+    ulogP[2 * (size_t)uN + 1] = old;
+    ++uN;
+  }
+  GWA_HD void ulogHeap(int i) {
+    if (DPM == 2 && uOn) ulogPut((uint64_t)(uint32_t)i, hslot(i));
+  }
   GWA_HD uint64_t &hslot(int i) const {
     if (HY) return i < L.heapH ? L.heapL[(size_t)i * L.hsL] : L.heapG[i];
     return L.heap()[(size_t)i * L.hs];
@@ -991,17 +1005,23 @@ struct BsfLane {
     for (int d = MAXD - 1; d >= 0; --d) t = (d >= depth || ek >= (av[d] >> KS)) ? d : t;
 #pragma unroll
     for (int d = 0; d < MAXD; ++d)
-      if (d < t) hslot(d == 0 ? kk : ai[d - 1]) = av[d];
+      if (d < t) {
+        const int w = d == 0 ? kk : ai[d - 1];
+        ulogHeap(w);
+        hslot(w) = av[d];
+      }
     int pos = t == 0 ? kk : pick(ai, t - 1);
     if (t == MAXD) {  // deeper than MAXD levels (large tiers only): Java's loop from there
       while (pos > 0) {
         const int parent = (pos - 1) >> 1;
         const uint64_t p = hslot(parent);
         if (ek >= (p >> KS)) break;
+        ulogHeap(pos);
         hslot(pos) = p;
         pos = parent;
       }
     }
+    ulogHeap(pos);
     hslot(pos) = e;
     tr(9, (uint32_t)(e & IDXM), (uint32_t)kk, (uint32_t)pos);
   }
@@ -1029,6 +1049,7 @@ struct BsfLane {
         if (xk <= (cv >> KS)) {
           go = 0;
         } else {
+          ulogHeap(kk);
           hslot(kk) = cv;
           kk = c + right;
           go = kk < half;
@@ -1042,12 +1063,14 @@ struct BsfLane {
           if (xk <= (dv >> KS)) {
             go = 0;
           } else {
+            ulogHeap(kk);
             hslot(kk) = dv;
             kk = c2 + right2;
             go = kk < half;
           }
         }
       }
+      ulogHeap(kk);
       hslot(kk) = x;
     }
     tr(10, (uint32_t)(result & IDXM), (uint32_t)heapSize, (uint32_t)(x & IDXM));
@@ -2156,7 +2179,10 @@ struct BsfLane {
   // split and clip children's 4 when it was the last candidate; or a first child and its run-ahead's
   // last state) and, net of a poll (xMode 0), 2 more queue entries; 3 from the next child (1).  0 when
   // there is room, else the OV_* capacity that may run out.
+  // (DPM 1, the first tier's kernel: no suspension at all -- its overflows restart on the next tier,
+  // as the suspend paths cost that kernel's register budget more than its few overflows' reruns)
   GWA_HD int passRoom() const {
+    if (DPM == 1) return 0;
     const int q = xMode == 1 ? 3 : 2;
     return nStates + 5 > caps.arena ? OV_ARENA : heapSize + q > caps.heap ? OV_HEAP : 0;
   }
@@ -2169,14 +2195,14 @@ struct BsfLane {
     return st == SS_REPORT ? LP_WAIT : st == SS_DONE ? LP_FINISH : LP_RUN;
   }
   GWA_HD int laneReport() {
-    if (listSize >= caps.list) {
+    if (DPM != 1 && listSize >= caps.list) {
       ovfWhat |= OV_LIST;
       susPhase = LP_WAIT;
       return LP_SUSPEND;
     }
     const int h0 = nHits, c0 = nCigar, sw0 = numSW, vb0 = verifyBytes, sa0 = saReads, st0 = status;
     if (searchReport()) return LP_RUN;
-    if (status == ST_OVERFLOW && (ovfWhat & ~(OV_HITS | OV_CIGAR | OV_SLICE)) == 0) {
+    if (DPM != 1 && status == ST_OVERFLOW && (ovfWhat & ~(OV_HITS | OV_CIGAR | OV_SLICE)) == 0) {
       nHits = h0;  // (verify appended hits and CIGAR ops only; nothing else changed yet)
       nCigar = c0;
       numSW = sw0;

@@ -1206,7 +1206,8 @@ int gwa_batch_run(gwa_batch_t *b) {
       ResumeBufs rb{};
       if (!sf) {
         const uint64_t rstride = resumeBytesFor(b->R, caps);
-        const uint64_t cap = std::min<uint64_t>(n, std::min<uint64_t>(8ull << 30, budget / 4) / rstride);
+        // (the first tier's kernel does not suspend: its overflows restart on the next tier)
+        const uint64_t cap = tb == 0 ? 0 : std::min<uint64_t>(n, std::min<uint64_t>(8ull << 30, budget / 4) / rstride);
         if (resOut.bytes < cap * rstride) {
           batchFree(resOut.p, s);
           resOut.p = nullptr;

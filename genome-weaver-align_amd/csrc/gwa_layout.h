@@ -110,6 +110,9 @@ constexpr int kStairLdsWords = 2048;  // 16 KiB of LDS per workgroup
 constexpr int kMaxReadLen = 512;
 constexpr int kLdsHeap = 8;           // first-tier priority-queue capacity (entries, in LDS)
 constexpr int kDeepLdsHeap = 8192;    // LDS queue entries per workgroup of a sparse deep tier (64 KiB)
+constexpr int kSfLdsHeap = 2048;      // -m sf cooperative kernel: LDS queue entries per wavefront (4 per workgroup)
+constexpr int kSfDJobs = 63;          // -m sf cooperative kernel: deferred verifications per pass (lanes 1-63)
+constexpr int kSfULog = 32768;        // -m sf cooperative kernel: undo-log entries (16 B) per read
 
 // ---- per-read output ----
 enum : int32_t {

@@ -58,9 +58,11 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
 #ifndef GWA_SEARCH_WAVES
 #define GWA_SEARCH_WAVES 2
 #endif
-// RES: the tier may resume reads from records (tiers >= 1; the first tier only suspends: the resume
-// path's register pressure is kept out of the kernel that runs most reads)
-template <int R, int QW, int LH, bool RES>
+// RES: 0 = the first tier (no suspension, no resume: BsfLane DPM 1), 1 = suspends and resumes reads
+// from records, 2 = suspends only (a tier whose input has no records: the second, after a first tier
+// that does not suspend).  The suspend / resume paths' register pressure is kept out of the kernels
+// that run most reads (C4 first tier 172 -> 107 ms without them).
+template <int R, int QW, int LH, int RES>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SEARCH_WAVES))) bsf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads,
                                                          const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                                                          uint64_t laneStride, Caps caps, OutHeader *oh, OutSlots os,
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   }
   // hybrid heap: k >= 4 with the LDS heap, sparse tiers; the first tier's kernel (LH 1 without resume)
   // keeps the DP slice (BsfLane DPM)
-  typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8)), 24, (LH == 1 && !RES) ? 1 : 0> Lane;
+  typedef BsfLane<R, QW, (LH == 2 || (LH != 0 && R >= 8)), 24, RES == 0 ? 1 : 0> Lane;
   Lane lane(ix, cfg, st, L, caps);
 #ifdef GWA_PROF
   lane.profG = prof;
@@ -153,7 +155,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
           lane.initRead(reads.codes + o, m);
           // a read the previous tier suspended continues from its record (Lane::resumeFrom, below)
           lane.buildMasks();
-          const bool rec = RES && res.in && i < res.inCap && lane.resumeValid(res.in + (size_t)i * res.inStride, r);
+          const bool rec = RES == 1 && res.in && i < res.inCap && lane.resumeValid(res.in + (size_t)i * res.inStride, r);
           if (rec) {
             resIdx = i;
             phase = RESUME;
@@ -166,7 +168,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
       }
     }
     if (__ballot(phase != EXHAUSTED) == 0) break;
-    if (RES && phase == RESUME) {
+    if (RES == 1 && phase == RESUME) {
       int rp = 0;
       lane.resumeFrom(res.in + (size_t)resIdx * res.inStride, r, &rp, false);
       phase = rp == Lane::LP_WAIT ? WAIT : RUN;
@@ -219,10 +221,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
 
 // sf_search<R, QW>: persistent lanes over the read list, one read per lane per iteration (lanes take
 // reads from a shared counter, one atomic per wavefront); overflowing reads go to the next tier.
-// COOP (the sparse last tier, caps.sparse = 64): one read per wavefront, lane 0 searching and the
-// whole wavefront verifying -- lane 0 its due candidate, lanes 1-63 speculatively the candidates at
-// the top of its queue (SfLane::specJob); whole-column DP history (a lone traceback of tens of edits
-// would recompute a column per edit), one wave per SIMD (the few wavefronts need no occupancy).
+// COOP (the sparse last tier, caps.sparse = 64): one read per wavefront, lane 0 searching and
+// deferring its verifications, lanes 1-63 running them in passes of up to 63 (SfLane: deferred
+// verification, roll-back when a result would lower minMismatches); its queue top in LDS,
+// whole-column DP history (a lone traceback of tens of edits would recompute a column per edit), one
+// wave per SIMD (the few wavefronts need no occupancy).
 template <int R, int QW, bool WRAP, bool COOP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? 1 : GWA_SEARCH_WAVES)))
 sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads, const uint32_t *list, uint32_t n,
@@ -243,6 +246,13 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
     __syncthreads();
   }
   __shared__ uint64_t qwLds[2 * QW * 256];
+  // COOP: each wavefront's (one read's) queue entries [0, kSfLdsHeap) in LDS
+  __shared__ uint64_t sfHeapLds[COOP ? 4 * kSfLdsHeap : 1];
+  if (COOP) {
+    L.heapL = sfHeapLds + (threadIdx.x >> 6) * kSfLdsHeap;
+    L.hsL = 1;
+    L.heapH = kSfLdsHeap;
+  }
   SfLane<R, QW, WRAP, COOP ? 2 : 0> lane(ix, cfg, st, L, caps);
   lane.chrRank = chrRank;
 #ifdef GWA_PROF
@@ -287,31 +297,61 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
         __threadfence_block();
         int run = 0;
         if (lid == 0) run = lane.sfBegin(false) ? 1 : 0;
-        else lane.buildMasks();  // (the helpers' DP reads the query words from their LDS rows)
+        else lane.buildMasks();  // (the helpers' DPs read the query words from their LDS rows)
+        decltype(lane) snap = lane;  // lane 0: its registers where the current deferral began
         for (;;) {
           int need = 0;
           if (lid == 0 && run) {
             int stp = 1;
-            while (stp == 1) stp = lane.template sfStepT<true>();
+            while (stp == 1 || stp == 3) {
+              stp = lane.template sfStepT<true>();
+              if (stp == 3) {
+                laneCopy(snap, lane);
+                lane.dMode = 1;
+                lane.uOn = 1;
+                stp = 1;
+              }
+            }
             need = stp == 2 ? 1 : 0;
             run = need;
           }
           need = __shfl(need, 0);
           if (!need) break;
-          const int hn = __shfl(lane.heapSize, 0), mm = __shfl(lane.minMismatches, 0), bs = __shfl(lane.bestScore, 0);
-          const bool job = lid == 0 || lane.specJob(lid, hn, mm, bs);
-          int rr = -1, pos = 0, diff = 0, co = 0, cl = 0;
-          if (job) {
-            if (lid != 0) {
-              lane.nCigar = 0;
-              lane.status = ST_UNMAPPED;
-            }
-            rr = lane.alignBlockDetailed(lane.jStrand, 0, m, lane.jRefStart, lane.jRefEnd, &pos, &diff, &co, &cl,
-                                         lid ? hcg : nullptr, lid ? hcap : 0);
-            if (lid != 0) lane.specPut(rr, pos, diff, co, cl, hcg);
+          __threadfence_block();
+          // the pass: lane j (1..63) runs queued job j - 1 into the result table
+          const int qn = __shfl(lane.dN, 0);
+#ifdef GWA_PROF
+          const uint64_t tpass = clock64();
+          if (lid == 0) prof[PR_NVW] += 1;
+#endif
+          if (lid != 0 && lane.djobLoad(lid - 1, qn)) {
+#ifdef GWA_PROF
+            prof[PR_NVL] += 1;
+#endif
+            int pos = 0, diff = 0, co = 0, cl = 0;
+            lane.nCigar = 0;
+            lane.status = ST_UNMAPPED;
+            const int rr = lane.alignBlockDetailed(lane.jStrand, 0, m, lane.jRefStart, lane.jRefEnd, &pos, &diff, &co, &cl,
+                                                   hcg, hcap);
+            lane.specPut(rr, pos, diff, co, cl, hcg);
           }
           __threadfence_block();
-          if (lid == 0) run = lane.candEnd(rr, pos, diff, co, cl) ? 1 : 0;
+#ifdef GWA_PROF
+          if (lid == 0) prof[PR_REPORT] += clock64() - tpass;
+#endif
+          if (lid == 0) {
+            bool go = true;
+            if (lane.dCommit(&go) >= 0) {  // a result lowers minMismatches: back to the deferral's start
+#ifdef GWA_PROF
+              prof[PR_NBW] += 1;
+#endif
+              lane.undoApply();
+              laneCopy(lane, snap);
+              lane.dN = 0;
+              go = lane.candFinish();  // (its job: the first deferred one, now in the table)
+            }
+            run = go ? 1 : 0;
+          }
         }
         if (lid == 0) {
           lane.writeSearchOutput(h, os, r);
@@ -397,10 +437,11 @@ void launchSearchQR(int ldsHeap, uint32_t lanes, const IndexView &ix, const Sear
 #define GWA_CASE(LL, RR)                                                                                               \
   hipLaunchKernelGGL((bsf_search_kernel<R, QW, LL, RR>), grid, dim3(256), 0, s, ix, cfg, st, reads, sres, list, n,     \
                      scratch, laneStride, caps, oh, os, chrRank, work, ovfList, ovfCount, ovfBits, res, trace, traceRead)
-  if (ldsHeap == 2) GWA_CASE(2, true);
-  else if (ldsHeap && (res.in || !caps.dpSlice)) GWA_CASE(1, true);  // (LH 1 without resume: the first tier only)
-  else if (ldsHeap) GWA_CASE(1, false);
-  else GWA_CASE(0, true);
+  if (ldsHeap == 2) GWA_CASE(2, 1);
+  else if (ldsHeap && caps.dpSlice) GWA_CASE(1, 0);  // the first tier
+  else if (ldsHeap && res.in) GWA_CASE(1, 1);
+  else if (ldsHeap) GWA_CASE(1, 2);
+  else GWA_CASE(0, 1);
 #undef GWA_CASE
 }
 

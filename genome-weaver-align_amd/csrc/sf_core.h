@@ -9,9 +9,18 @@
 //   AlignmentResultHolder.add (:369-389); the report selection of align (:165-222) is
 //   BsfLane::writeSearchOutput (the same code in the reference).
 #pragma once
+#include <new>
 #include "bsf_core.h"
 
 namespace gwa {
+
+// dst = src for lane objects (their IndexView / SearchConfig / StairTables members are references,
+// the same objects in both: copy-construction in place; the cooperative kernel's register snapshot)
+template <class T>
+GWA_HD void laneCopy(T &dst, const T &src) {
+  dst.~T();
+  ::new (static_cast<void *>(&dst)) T(src);
+}
 
 // SFState (S/SuffixFilter.java:414-471).  si: rows [lb, ub) of the forward-extension index
 // (FMIndexOnGenome.forwardSearch, A/FMIndexOnGenome.java:138-141,203-209); with M_TEXT in meta the
@@ -53,10 +62,11 @@ GWA_HD bool sfChunksWrap(int m_, int kk) {
 
 // WRAP: the batch has reads whose chunk starts wrap (sfChunksWrap); without them the automaton's
 // out-of-table mask path is compiled out (it cost the R = 8 kernel ~35 spilled VGPRs)
-// DPM: the DP history mode (BsfLane); the cooperative sparse kernel keeps whole columns (2)
+// DPM: the DP history mode (BsfLane); the cooperative sparse kernel keeps whole columns (2) and the
+// top of its queue in LDS (BsfLane's hybrid heap: L.heapL / heapH, set by the kernel)
 template <int R, int QW, bool WRAP = true, int DPM = 0>
-struct SfLane : BsfLane<R, QW, false, 24, DPM> {
-  typedef BsfLane<R, QW, false, 24, DPM> B;
+struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
+  typedef BsfLane<R, QW, DPM == 2, 24, DPM> B;
   using B::ix;
   using B::cfg;
   using B::L;
@@ -112,6 +122,7 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
   }
   GWA_HD void sfFree(int id) {
     if (spare >= 0) {
+      if (DPM == 2 && B::uOn) B::ulogPut(kUArena | (uint32_t)spare, arena()[spare].lb);
       arena()[spare].lb = (uint32_t)freeHead;
       freeHead = spare;
     }
@@ -137,6 +148,7 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
       for (int i = 0; i < nCand; ++i)
         if (c[i] == key) return 0;
       if (nCand >= caps.cand) return -1;
+      if (DPM == 2 && B::uOn) B::ulogPut(kUCand | (uint32_t)nCand, (uint64_t)c[nCand]);
       c[nCand++] = key;
       return 1;
     }
@@ -149,29 +161,10 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
       h = (h + 1u) & mask;
     }
     if (2 * (nCand + 1) > caps.cand) return -1;
+    if (DPM == 2 && B::uOn) B::ulogPut(kUCand | h, (uint64_t)c[h]);
     c[h] = key;
     ++nCand;
     return 1;
-  }
-
-  // candidates[strand].contains(start), without adding it (the helper lanes of the cooperative kernel)
-  GWA_HD bool candHas(int64_t key) const {
-    const int64_t *c = L.cand();
-    if (caps.cand < kCandHash) {
-      int hit = 0;
-      for (int i = 0; i < nCand; ++i) hit |= c[i] == key ? 1 : 0;
-      return hit != 0;
-    }
-    const uint32_t mask = (uint32_t)caps.cand - 1u;
-    uint32_t h = (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ULL) >> 40) & mask;
-    int found = 0, go = 1;
-    for (int q = 0; go && q < caps.cand; ++q) {
-      const int64_t v = c[h];
-      found = v == key ? 1 : 0;
-      go = (found == 0 && v != kCandEmpty) ? 1 : 0;
-      h = (h + 1u) & mask;
-    }
-    return found != 0;
   }
 
   // SFState.compareTo (:463-469) as a heap key: kOffset ascending, then score descending
@@ -191,6 +184,11 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
     d.kOffset = (uint8_t)kOffset; d.hasHit = hasHit ? 1 : 0; d.meta = meta;
 #pragma unroll
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nrows ? rows[i] : 0ULL;
+    if (DPM == 2 && B::uOn) {  // (a recycled slot may be a state polled during the deferral: its words)
+      const uint64_t *w = (const uint64_t *)(arena() + id);
+      for (int q = 0; q < (int)(sizeof(SfState<R>) / 8); ++q)
+        B::ulogPut(kUWord | ((uint64_t)id * (sizeof(SfState<R>) / 8) + q), w[q]);
+    }
     arena()[id] = d;
     return id;
   }
@@ -407,49 +405,70 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
     return candEnd(r, pos, diff, co, cl);
   }
 
-  // ---- speculative verification (the cooperative kernel of the sparse last tier) ----
-  // Lane 0 of a wavefront runs the read's search; when a verification is due whose result is not in
-  // the speculation table, the whole wavefront runs DPs: lane 0 its own, lanes 1-63 those of the
-  // single-row states at queue entries 1-63 -- the next polls, mostly -- that the owner would verify
-  // when polled (the cutoff thresholds only tighten, so a state cut now is cut then) and whose start
-  // is neither verified nor speculated yet.  A result is a pure function of the job, so taking it
-  // from the table when the owner reaches the candidate changes nothing but the time.  Table entry:
-  // the key, the result and a CIGAR of up to 20 ops (longer ones are not kept); open addressing with
-  // at most kSpecProbe probes, slots claimed by compare-and-swap.
+  // ---- deferred verification (the cooperative kernel of the sparse last tier, DPM 2) ----
+  // Lane 0 of a wavefront runs the read's search.  A verification whose result is not in the result
+  // table is not waited for: it is queued -- with every later one, in poll order -- and the search
+  // goes on with its writes to the queue, the arena's free links and the candidate set logged (undo
+  // log).  At kSfDJobs queued jobs, at the search's end or when the log is nearly full, lanes 1-63
+  // run the queued DPs into the table and lane 0 commits the jobs in order (candEnd).  A
+  // verification acts on the search only through minMismatches / bestScore (the cutoff, :261): if a
+  // committed result would lower them while something was polled after its job, the search is put
+  // back to where the deferral began (the undo log, and the copy of the lane's registers the kernel
+  // took there) and goes on from that point, taking every result it meets from the table.
+  // minMismatches only decreases, so a read rolls back at most k + 1 times.  A DP result is a pure
+  // function of (start, strand): taking it from the table changes nothing but the time.
+  // Table entry: the key, the result and a CIGAR of up to kSpecOps ops (a longer one is recomputed
+  // by lane 0 when it commits); open addressing, <= kSpecProbe probes, slots claimed by CAS.
   struct SpecEntry {
     int64_t key;
     int32_t r, diff, pos;
     uint16_t ncig, pad;
     uint16_t ops[20];
   };
+  struct DJob {
+    int64_t key, refStart, refEnd;
+    int32_t strand;
+    uint32_t popsAt;  // polls of the read when the job was queued
+  };
   static constexpr int kSpecOps = 20, kSpecProbe = 32;
+  // undo-log tags: 0 a queue slot, kUArena a free link, kUCand a candidate-set slot, kUWord an arena word
+  static constexpr uint64_t kUArena = 1ULL << 62, kUCand = 2ULL << 62, kUWord = 3ULL << 62;
+  int dMode = 0, dN = 0;  // deferring; jobs queued
+  uint32_t dPops = 0;     // polls so far
   GWA_HD SpecEntry *spec() const { return (SpecEntry *)(L.slice + L.oSpec); }
+  GWA_HD DJob *djobs() const { return (DJob *)(L.slice + L.oSpec + 64 * (size_t)caps.spec); }
+  GWA_HD uint64_t *ulogBase() const {
+    return (uint64_t *)(L.slice + L.oSpec + 64 * (size_t)caps.spec + sizeof(DJob) * (size_t)kSfDJobs);
+  }
   GWA_HD uint32_t specSlot(int64_t key) const {
     return (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ULL) >> 40) & ((uint32_t)caps.spec - 1u);
   }
-  // the owner: the result of job jKey from the table, with alignBlockDetailed's effects (counters,
-  // CIGAR appended); false = not there
-  GWA_HD bool specTake(int *r, int *pos, int *diff, int *co, int *cl) {
-    uint32_t h = specSlot(jKey);
+  // the table slot holding key, or -1
+  GWA_HD int specFind(int64_t key) const {
+    uint32_t h = specSlot(key);
     int at = -1, go = 1;
     for (int q = 0; go && q < kSpecProbe; ++q) {
       const int64_t v = spec()[h].key;
-      at = v == jKey ? (int)h : -1;
+      at = v == key ? (int)h : -1;
       go = (at < 0 && v != kCandEmpty) ? 1 : 0;
       h = (h + 1u) & ((uint32_t)caps.spec - 1u);
     }
-    if (at < 0) return false;
+    return at;
+  }
+  // the job's verification from table slot at, with alignBlockDetailed's effects (counters, CIGAR
+  // ops appended); *r as alignBlockDetailed returns it
+  GWA_HD void specApply(int at, int *r, int *pos, int *diff, int *co, int *cl) {
     const SpecEntry &e = spec()[at];
     const int N = (int)(jRefEnd - jRefStart), bMax = (m + 63) / 64 > 0 ? (m + 63) / 64 : 1;
     ++numSW;
     verifyBytes += (2 * N + 7) / 8 + (N + 7) / 8 + 32 * bMax;
     *r = e.r;
-    if (e.r != 0) return true;
+    if (e.r != 0) return;
     const int n = e.ncig;
     if (nCigar + n + 4 > caps.cigar) {
       B::ovf(OV_CIGAR);
       *r = -1;
-      return true;
+      return;
     }
     for (int i = 0; i < n; ++i) L.cigar()[nCigar + i] = e.ops[i];
     *co = nCigar;
@@ -457,39 +476,14 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
     nCigar += n;
     *pos = e.pos;
     *diff = e.diff;
-    return true;
   }
-  // a helper lane (lane j of the owner's wavefront, sharing its slice): its job from queue entry j of
-  // the owner's queue of hn entries at thresholds mm / bs; false = none
-  GWA_HD bool specJob(int j, int hn, int mm, int bs) {
-    if (j >= hn) return false;
-    const int idx = (int)(L.heapP[j] & ((1ULL << 24) - 1ULL));  // (KS = 24; the slice heap, hs = 1)
-    const SfState<R> *p = arena() + idx;
-    const uint32_t lb = p->lb, ub = p->ub;
-    const int score = p->score, offset = p->offset, index = p->index;
-    const int strand = p->strand, kOffset = p->kOffset;
-    const uint8_t meta = p->meta;
-    const int ubScore = score + (offset + (m - index)) * cfg.matchScore;
-    if (kOffset > mm || ubScore < bs || ub - lb != 1) return false;
-    int64_t key;
-    const int64_t start = candStart(lb, strand, index, meta, &key);
-    const int64_t refStart = start - k > 0 ? start - k : 0;
-    const int64_t refEnd = start + m + k < (int64_t)ix.N ? start + m + k : (int64_t)ix.N;
-    if (refStart > refEnd || candHas(key)) return false;
-    uint32_t h = specSlot(key);
-    int go = 1, seen = 0;
-    for (int q = 0; go && q < kSpecProbe; ++q) {
-      const int64_t v = spec()[h].key;
-      seen = v == key ? 1 : 0;
-      go = (seen == 0 && v != kCandEmpty) ? 1 : 0;
-      h = (h + 1u) & ((uint32_t)caps.spec - 1u);
-    }
-    if (seen) return false;
-    jStrand = strand;
-    jRefStart = refStart;
-    jRefEnd = refEnd;
-    jKey = key;
-    return true;
+  // the job (jKey ...): its result from the table, or its DP run here; then candEnd
+  GWA_HD bool candFinish() {
+    int r = 0, pos = 0, diff = 0, co = 0, cl = 0;
+    const int at = specFind(jKey);
+    if (at >= 0) specApply(at, &r, &pos, &diff, &co, &cl);
+    else r = B::alignBlockDetailed(jStrand, 0, m, jRefStart, jRefEnd, &pos, &diff, &co, &cl);
+    return candEnd(r, pos, diff, co, cl);
   }
   // a helper lane: keep its result (r >= 0; a CIGAR of <= kSpecOps ops, from its own area cg)
   GWA_HD void specPut(int r, int pos, int diff, int co, int cl, const uint16_t *cg) {
@@ -516,12 +510,73 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
     e.ncig = (uint16_t)(r == 0 ? cl : 0);
     for (int i = 0; r == 0 && i < cl; ++i) e.ops[i] = cg[co + i];
   }
-  // the candidate set and the speculation table emptied by the 64 lanes of the wavefront together
+  // a helper lane (1..63): load queued job lid - 1 of the owner (sharing its slice); false = none, or
+  // its result is already in the table
+  GWA_HD bool djobLoad(int j, int qn) {
+    if (j >= qn) return false;
+    const DJob jb = djobs()[j];
+    jKey = jb.key;
+    jStrand = jb.strand;
+    jRefStart = jb.refStart;
+    jRefEnd = jb.refEnd;
+    return specFind(jKey) < 0;
+  }
+  // the candidate set and the result table emptied by the 64 lanes of the wavefront together
   GWA_HD void coopClear(int lid) {
     nCand = 0;
+    dMode = dN = 0;
+    dPops = 0;
+    B::uN = B::uOn = 0;
+    B::ulogP = ulogBase();
     if (caps.cand >= kCandHash)
       for (int i = lid; i < caps.cand; i += 64) L.cand()[i] = kCandEmpty;
     for (int i = lid; i < caps.spec; i += 64) spec()[i].key = kCandEmpty;
+  }
+  // lane 0 after a pass: commit the queued jobs in order.  Returns -1 when all were committed (*go
+  // false: the search ended), else the job at which the search must roll back.
+  GWA_HD int dCommit(bool *go) {
+    *go = true;
+    int rb = -1;
+    for (int i = 0; i < dN && rb < 0 && *go; ++i) {
+      const DJob jb = djobs()[i];
+      jKey = jb.key;
+      jStrand = jb.strand;
+      jRefStart = jb.refStart;
+      jRefEnd = jb.refEnd;
+      const int at = specFind(jKey);
+      int r = 0, pos = 0, diff = 0, co = 0, cl = 0;
+      if (at >= 0) {
+        r = spec()[at].r;
+        pos = spec()[at].pos;
+        diff = spec()[at].diff;
+      } else {  // (not kept: its DP here, in order; rolled back below if need be)
+        r = B::alignBlockDetailed(jStrand, 0, m, jRefStart, jRefEnd, &pos, &diff, &co, &cl);
+      }
+      int32_t chr, p;
+      const bool lower = r == 0 && m > 0 && diff < minMismatches && B::translate(jRefStart + pos + 1, &chr, &p) == 0;
+      if (lower && (i + 1 < dN || dPops > jb.popsAt)) {
+        rb = i;
+      } else {
+        if (at >= 0) specApply(at, &r, &pos, &diff, &co, &cl);
+        *go = candEnd(r, pos, diff, co, cl);
+      }
+    }
+    B::uOn = 0;  // (a roll-back then replays the log: undoApply)
+    if (rb < 0) dMode = dN = B::uN = 0;
+    return rb;
+  }
+  // the logged writes undone, newest first (the kernel then restores the registers)
+  GWA_HD void undoApply() {
+    for (int i = B::uN - 1; i >= 0; --i) {
+      const uint64_t tag = B::ulogP[2 * (size_t)i], old = B::ulogP[2 * (size_t)i + 1];
+      const uint32_t at = (uint32_t)tag;
+      const uint64_t kind = tag >> 62;
+      if (kind == 0) B::hslot((int)at) = old;
+      else if (kind == 1) arena()[at].lb = (uint32_t)old;
+      else if (kind == 2) L.cand()[at] = (int64_t)old;
+      else ((uint64_t *)arena())[tag & ((1ULL << 62) - 1ULL)] = old;
+    }
+    B::uN = 0;
   }
 
   // SFState.nextState (:448-460) + ReadAlignmentNFA.nextState(nextACGTIndex, progress, m, ...)
@@ -549,15 +604,26 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
     return status != ST_OVERFLOW;
   }
 
-  // one iteration of the queue loop (:257-290): 0 = the loop ended, 1 = go on; COOP (the owner lane
-  // of the cooperative kernel): 2 = a verification is due (jStrand, jRefStart, jRefEnd) that the
-  // speculation table does not hold -- the wavefront runs it, then candEnd
+  // one iteration of the queue loop (:257-290): 0 = the loop ended, 1 = go on.  COOP (lane 0 of the
+  // cooperative kernel): 2 = run a pass over the queued jobs and commit them (dCommit); 3 = a job was
+  // queued and deferral begins here (the kernel copies the lane's registers, then sets dMode / uOn)
   template <bool COOP>
   GWA_HD int sfStepT() {
-    if (heapSize == 0 || status == ST_OVERFLOW || status == ST_ERROR) return 0;
+    const int end = COOP && dMode ? 2 : 0;
+    if (heapSize == 0 || status == ST_OVERFLOW || status == ST_ERROR) return end;
+    if (COOP && dMode && B::uN + 512 > kSfULog) return 2;  // (a step logs < 512 writes)
     GWA_PT(tp);
-    const int idx = B::queuePoll();
-    const SfState<R> c = arena()[idx];
+    int idx;
+    SfState<R> c;
+    if (COOP) {  // the root's state is loaded while the sift runs (its registers are free in that kernel)
+      idx = (int)(B::hslot(0) & ((1ULL << 24) - 1ULL));
+      c = arena()[idx];
+      B::queuePoll();
+      ++dPops;
+    } else {
+      idx = B::queuePoll();
+      c = arena()[idx];
+    }
     sfFree(idx);
     GWA_PC(PR_NSW, PR_NSL);
     GWA_PA(PR_POLL, tp);
@@ -569,10 +635,16 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
       if (COOP) {
         bool go;
         if (!candBegin(c, &go)) {
-          res = go ? 1 : 0;
+          res = go ? 1 : end;
+        } else if (!dMode && specFind(jKey) >= 0) {
+#ifdef GWA_PROF
+          if (profG) profG[PR_NBL] += 1;  // (results taken from the table outside a deferral)
+#endif
+          res = candFinish() ? 1 : 0;
         } else {
-          int r = 0, pos = 0, diff = 0, co = 0, cl = 0;
-          res = specTake(&r, &pos, &diff, &co, &cl) ? (candEnd(r, pos, diff, co, cl) ? 1 : 0) : 2;
+          djobs()[dN] = DJob{jKey, jRefStart, jRefEnd, jStrand, dPops};
+          ++dN;
+          res = !dMode ? 3 : dN >= kSfDJobs ? 2 : 1;
         }
       } else {
         res = addCandidate(c) ? 1 : 0;
@@ -587,11 +659,12 @@ struct SfLane : BsfLane<R, QW, false, 24, DPM> {
     B::rank2(fm, c.lb, c.ub, lo, hi);
     GWA_PA(PR_FM, tf);
     ++numFMIndexSearches;
+    int ok = 1;
     for (int ch = 0; ch < 4; ++ch) {  // ACGT.exceptN
       const uint64_t l = ix.C[ch] + lo[ch], u = ix.C[ch] + hi[ch];
-      if (l < u && !child(c, ch, (uint32_t)l, (uint32_t)u)) return 0;
+      if (ok && l < u && !child(c, ch, (uint32_t)l, (uint32_t)u)) ok = 0;
     }
-    return 1;
+    return ok ? 1 : end;
   }
   GWA_HD bool sfStep() { return sfStepT<false>() != 0; }
 

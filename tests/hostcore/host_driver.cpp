@@ -25,7 +25,7 @@ struct HC {
 };
 
 static uint64_t g_suspends = 0;  // reads suspended (and resumed on the next tier), all calls
-static uint64_t g_specJobs = 0, g_specMiss = 0, g_specTaken = 0;  // HC_SF_COOP: helper verifications, the owner's own, taken from the table
+static uint64_t g_specJobs = 0, g_specMiss = 0, g_specTaken = 0;  // HC_SF_COOP: helper verifications, passes, roll-backs
 
 // the GPU's capacity tiers (gwa_api.cpp kTiers) replayed on the CPU
 template <int R, int QW>
@@ -77,6 +77,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
       if (t == 0 && getenv("HC_T0_HITS")) { bc.hits = bc.list = atoi(getenv("HC_T0_HITS")); bc.cigar = 16 * bc.hits; }  // experiments
       if (t == 1 && getenv("HC_T1_HITS")) { bc.hits = bc.list = atoi(getenv("HC_T1_HITS")); bc.cigar = 16 * bc.hits; }
       if (t == 0 && getenv("HC_T0_ARENA")) { bc.arena = bc.heap = atoi(getenv("HC_T0_ARENA")); }
+      if (t == 1 && getenv("HC_T1_ARENA")) { bc.arena = bc.heap = atoi(getenv("HC_T1_ARENA")); }
       if (t >= 4) {
         const int g = t - 3;
         for (Caps *c : {&sc, &bc}) {
@@ -121,34 +122,47 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         CL &o = ln[0];
         hd = OutHeader{};
         int run = o.sfBegin(false) ? 1 : 0;
-        int miss = 0;
+        CL snap = o;  // (the kernel's copy of lane 0's registers where a deferral began)
         for (;;) {
           int need = 0;
           if (run) {
             int stp = 1;
-            while (stp == 1) stp = o.template sfStepT<true>();
+            while (stp == 1 || stp == 3) {
+              stp = o.template sfStepT<true>();
+              if (stp == 3) {
+                laneCopy(snap, o);
+                o.dMode = 1;
+                o.uOn = 1;
+                stp = 1;
+              }
+            }
             need = stp == 2 ? 1 : 0;
             run = need;
           }
           if (!need) break;
+          ++g_specMiss;  // (passes)
+          const int qn = o.dN;
           for (int h = 1; h < 64; ++h) {
-            if (!ln[h].specJob(h, o.heapSize, o.minMismatches, o.bestScore)) continue;
+            if (!ln[h].djobLoad(h - 1, qn)) continue;
             int pos = 0, diff = 0, co = 0, cl = 0;
             ln[h].nCigar = 0;
             ln[h].status = ST_UNMAPPED;
             uint16_t *cg = hcig.data() + (size_t)h * hcap;
-            const int r = ln[h].alignBlockDetailed(ln[h].jStrand, 0, (int)mlen, ln[h].jRefStart, ln[h].jRefEnd, &pos, &diff, &co,
-                                                   &cl, cg, hcap);
+            const int r = ln[h].alignBlockDetailed(ln[h].jStrand, 0, (int)mlen, ln[h].jRefStart, ln[h].jRefEnd, &pos, &diff,
+                                                   &co, &cl, cg, hcap);
             ln[h].specPut(r, pos, diff, co, cl, cg);
             ++g_specJobs;
           }
-          int pos = 0, diff = 0, co = 0, cl = 0;
-          const int r = o.alignBlockDetailed(o.jStrand, 0, (int)mlen, o.jRefStart, o.jRefEnd, &pos, &diff, &co, &cl);
-          ++g_specMiss;
-          ++miss;
-          run = o.candEnd(r, pos, diff, co, cl) ? 1 : 0;
+          bool go = true;
+          if (o.dCommit(&go) >= 0) {
+            ++g_specTaken;  // (roll-backs)
+            o.undoApply();
+            laneCopy(o, snap);
+            o.dN = 0;
+            go = o.candFinish();
+          }
+          run = go ? 1 : 0;
         }
-        g_specTaken += (uint64_t)(o.numSW - miss);
         used[0] = used[1] = used[2] = 0;
         o.writeSearchOutput(&hd, os, 0);
         hd.quickSteps = o.quickSteps;

@@ -79,8 +79,7 @@ def suspends():
 
 
 def spec_stats():
-    """HC_SF_COOP runs so far: (helper-lane speculative verifications, verifications the owner ran
-    itself, verifications the owner took from the speculation table)"""
+    """HC_SF_COOP runs so far: (verifications run by helper lanes, passes, roll-backs)"""
     v = (ctypes.c_uint64 * 3)()
     lib().hc_spec_stats(v)
     return int(v[0]), int(v[1]), int(v[2])
