@@ -907,7 +907,8 @@ struct BsfLane {
   // top slots and the slice beyond them -- one flat address either way
   // Undo log of the queue's writes (DPM 2: the cooperative -m sf kernel's deferred verification,
   // SfLane): while uOn, every queue slot written is logged first as (slot, old entry), so the
-  // queue can be put back as it was when the deferral began
+  // queue can be put back as it was when the deferral began.  The old entries are values the sifts
+  // hold anyway (no extra loads); a poll logs its vacated last slot, so an offer's new slot needs none.
   uint64_t *ulogP = nullptr;
   int uN = 0, uOn = 0;
   GWA_HD void ulogPut(uint64_t tag, uint64_t old) {
@@ -915,8 +916,8 @@ struct BsfLane {
     ulogP[2 * (size_t)uN + 1] = old;
     ++uN;
   }
-  GWA_HD void ulogHeap(int i) {
-    if (DPM == 2 && uOn) ulogPut((uint64_t)(uint32_t)i, hslot(i));
+  GWA_HD void ulogHeap(int i, uint64_t old) {
+    if (DPM == 2 && uOn) ulogPut((uint64_t)(uint32_t)i, old);
   }
   GWA_HD uint64_t &hslot(int i) const {
     if (HY) return i < L.heapH ? L.heapL[(size_t)i * L.hsL] : L.heapG[i];
@@ -1007,21 +1008,23 @@ struct BsfLane {
     for (int d = 0; d < MAXD; ++d)
       if (d < t) {
         const int w = d == 0 ? kk : ai[d - 1];
-        ulogHeap(w);
+        if (d > 0) ulogHeap(w, av[d - 1]);
         hslot(w) = av[d];
       }
     int pos = t == 0 ? kk : pick(ai, t - 1);
+    uint64_t cur = t == 0 ? 0ULL : pick(av, t - 1);  // the entry at pos (t > 0)
     if (t == MAXD) {  // deeper than MAXD levels (large tiers only): Java's loop from there
       while (pos > 0) {
         const int parent = (pos - 1) >> 1;
         const uint64_t p = hslot(parent);
         if (ek >= (p >> KS)) break;
-        ulogHeap(pos);
+        ulogHeap(pos, cur);
         hslot(pos) = p;
         pos = parent;
+        cur = p;
       }
     }
-    ulogHeap(pos);
+    if (t > 0) ulogHeap(pos, cur);
     hslot(pos) = e;
     tr(9, (uint32_t)(e & IDXM), (uint32_t)kk, (uint32_t)pos);
   }
@@ -1030,9 +1033,11 @@ struct BsfLane {
     int s = --heapSize;
     const uint64_t result = hslot(0);
     const uint64_t x = hslot(s);
+    ulogHeap(s, x);  // (a later offer reuses the vacated slot)
     if (s != 0) {
       const int n = heapSize, half = n >> 1, capm1 = caps.heap - 1;
       int kk = 0;
+      uint64_t cur = result;  // the entry at kk (the undo log's old value)
       const uint64_t xk = x >> KS;
       int go = kk < half;  // single-exit loop (no break): see quickScan
       while (go) {
@@ -1049,8 +1054,9 @@ struct BsfLane {
         if (xk <= (cv >> KS)) {
           go = 0;
         } else {
-          ulogHeap(kk);
+          ulogHeap(kk, cur);
           hslot(kk) = cv;
+          cur = cv;
           kk = c + right;
           go = kk < half;
         }
@@ -1063,14 +1069,15 @@ struct BsfLane {
           if (xk <= (dv >> KS)) {
             go = 0;
           } else {
-            ulogHeap(kk);
+            ulogHeap(kk, cur);
             hslot(kk) = dv;
+            cur = dv;
             kk = c2 + right2;
             go = kk < half;
           }
         }
       }
-      ulogHeap(kk);
+      ulogHeap(kk, cur);
       hslot(kk) = x;
     }
     tr(10, (uint32_t)(result & IDXM), (uint32_t)heapSize, (uint32_t)(x & IDXM));

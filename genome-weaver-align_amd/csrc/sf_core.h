@@ -116,13 +116,13 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
     if (freeHead >= 0) {
       const int id = freeHead;
       freeHead = (int)arena()[id].lb;
+      if (DPM == 2 && B::uOn) B::ulogPut(kUArena | (uint32_t)id, (uint64_t)(uint32_t)freeHead);  // (its free link)
       return id;
     }
     return B::allocState();
   }
   GWA_HD void sfFree(int id) {
     if (spare >= 0) {
-      if (DPM == 2 && B::uOn) B::ulogPut(kUArena | (uint32_t)spare, arena()[spare].lb);
       arena()[spare].lb = (uint32_t)freeHead;
       freeHead = spare;
     }
@@ -148,8 +148,7 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
       for (int i = 0; i < nCand; ++i)
         if (c[i] == key) return 0;
       if (nCand >= caps.cand) return -1;
-      if (DPM == 2 && B::uOn) B::ulogPut(kUCand | (uint32_t)nCand, (uint64_t)c[nCand]);
-      c[nCand++] = key;
+      c[nCand++] = key;  // (past the restored nCand: no undo entry)
       return 1;
     }
     const uint32_t mask = (uint32_t)caps.cand - 1u;
@@ -161,7 +160,7 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
       h = (h + 1u) & mask;
     }
     if (2 * (nCand + 1) > caps.cand) return -1;
-    if (DPM == 2 && B::uOn) B::ulogPut(kUCand | h, (uint64_t)c[h]);
+    if (DPM == 2 && B::uOn) B::ulogPut(kUCand | h, (uint64_t)kCandEmpty);
     c[h] = key;
     ++nCand;
     return 1;
@@ -184,11 +183,6 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
     d.kOffset = (uint8_t)kOffset; d.hasHit = hasHit ? 1 : 0; d.meta = meta;
 #pragma unroll
     for (int i = 0; i < R; ++i) d.nfa[i] = i < nrows ? rows[i] : 0ULL;
-    if (DPM == 2 && B::uOn) {  // (a recycled slot may be a state polled during the deferral: its words)
-      const uint64_t *w = (const uint64_t *)(arena() + id);
-      for (int q = 0; q < (int)(sizeof(SfState<R>) / 8); ++q)
-        B::ulogPut(kUWord | ((uint64_t)id * (sizeof(SfState<R>) / 8) + q), w[q]);
-    }
     arena()[id] = d;
     return id;
   }
@@ -396,13 +390,44 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
     sfResultAdd(h, diff);
     return status != ST_OVERFLOW;
   }
+  // addCandidate (:298-343) in one piece (the per-lane kernels: locals, not the job fields)
   GWA_HD bool addCandidate(const SfState<R> &c) {
-    bool go;
-    if (!candBegin(c, &go)) return go;
+    if (c.ub - c.lb != 1) return true;  // multi hit: nothing (:339-342)
+    const int strand = c.strand;
+    int64_t key;
+    const int64_t start = candStart(c.lb, strand, c.index, c.meta, &key);
+    GWA_PT(tci);
+    const int ins = candInsert(key);
+    GWA_PA(PR_SPLIT, tci);
+    if (ins == 0) return true;  // candidates[strand].contains(start)
+    if (ins < 0) {
+      B::ovf(OV_CAND);
+      return false;
+    }
+    const int64_t refStart = start - k > 0 ? start - k : 0;
+    const int64_t refEnd = start + m + k < (int64_t)ix.N ? start + m + k : (int64_t)ix.N;
+    if (refStart > refEnd) {  // ACGTSequence.subString throws
+      status = ST_ERROR;
+      return false;
+    }
     int pos = 0, diff = 0, co = 0, cl = 0;
     GWA_PC(PR_NVW, PR_NVL);
-    const int r = B::alignBlockDetailed(jStrand, 0, m, jRefStart, jRefEnd, &pos, &diff, &co, &cl);
-    return candEnd(r, pos, diff, co, cl);
+    const int r = B::alignBlockDetailed(strand, 0, m, refStart, refEnd, &pos, &diff, &co, &cl);
+    if (r < 0) return false;
+    if (r == 1) return true;  // alignment == null
+    int32_t chr, p;
+    if (B::translate(refStart + pos + 1, &chr, &p) != 0) {  // UTGBException is logged
+      nCigar = co;
+      return true;
+    }
+    if (m == 0 || diff > minMismatches) {  // reportResult (:345-353)
+      nCigar = co;
+      return true;
+    }
+    const int h = B::newHit(chr, p, m, 0, m, diff, strand, co, cl, 1);
+    if (h < 0) return false;
+    sfResultAdd(h, diff);
+    return status != ST_OVERFLOW;
   }
 
   // ---- deferred verification (the cooperative kernel of the sparse last tier, DPM 2) ----
@@ -620,6 +645,12 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
       c = arena()[idx];
       B::queuePoll();
       ++dPops;
+      if (DPM == 2 && B::uOn) {  // the polled state's words: its slot may be reused before a roll-back
+        const uint64_t *w = (const uint64_t *)&c;
+#pragma unroll
+        for (int q = 0; q < (int)(sizeof(SfState<R>) / 8); ++q)
+          B::ulogPut(kUWord | ((uint64_t)idx * (sizeof(SfState<R>) / 8) + q), w[q]);
+      }
     } else {
       idx = B::queuePoll();
       c = arena()[idx];
