@@ -1115,8 +1115,9 @@ int gwa_batch_run(gwa_batch_t *b) {
         caps.list <<= gList;
         caps.cigar <<= gCigar;
         caps.cand <<= gCand;
-        // -m sf: the speculation table of the cooperative kernel (run when the tier is sparse, 64)
-        if (sf) caps.spec = caps.cand;
+        // -m sf: the result table of the cooperative kernel (run when the tier is sparse, 64);
+        // GWA_SF_COOP=0 runs the per-lane kernel there instead (A/B and diagnostics)
+        if (sf && !(getenv("GWA_SF_COOP") && atoi(getenv("GWA_SF_COOP")) == 0)) caps.spec = caps.cand;
       }
       // -m bsf, k >= 4 (R >= 8): the verification memo (bsf_core.h verify), twice the hit list's
       // entries, a power of two; k <= 3 reads do not repeat verifications (C2: 1431 of 1431 unique)

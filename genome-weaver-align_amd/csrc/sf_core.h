@@ -305,10 +305,14 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
       bestScore = m * cfg.matchScore - diff * cfg.mismatchPenalty;
     }
     if (maxMatchLength < m) maxMatchLength = m;
-    int n = lower ? 0 : listSize;
-    for (int i = 0; lower && i < listSize; ++i) {
-      const int e = L.list()[i];
-      if (L.hits()[e].diff <= minMismatches) L.list()[n++] = e;
+    int n = listSize;
+    if (lower) {  // (the scan in a branch of its own: a loop whose condition also tests the loop-invariant
+                  // flag lost hits on gfx950 -- tests/test_gpu_parity.py::test_long_reads_on_gpu, -m sf 400 bp)
+      n = 0;
+      for (int i = 0; i < listSize; ++i) {
+        const int e = L.list()[i];
+        if (L.hits()[e].diff <= minMismatches) L.list()[n++] = e;
+      }
     }
     if (n >= caps.list) {
       B::ovf(OV_LIST);
@@ -690,12 +694,11 @@ struct SfLane : BsfLane<R, QW, DPM == 2, 24, DPM> {
     B::rank2(fm, c.lb, c.ub, lo, hi);
     GWA_PA(PR_FM, tf);
     ++numFMIndexSearches;
-    int ok = 1;
     for (int ch = 0; ch < 4; ++ch) {  // ACGT.exceptN
       const uint64_t l = ix.C[ch] + lo[ch], u = ix.C[ch] + hi[ch];
-      if (ok && l < u && !child(c, ch, (uint32_t)l, (uint32_t)u)) ok = 0;
+      if (l < u && !child(c, ch, (uint32_t)l, (uint32_t)u)) return end;
     }
-    return ok ? 1 : end;
+    return 1;
   }
   GWA_HD bool sfStep() { return sfStepT<false>() != 0; }
 

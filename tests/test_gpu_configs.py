@@ -78,6 +78,31 @@ def hg19r_full(request):
     gi.close()
 
 
+class _Heartbeat:
+    """a line every 60 s while a long step runs (a silent GPU-box step is taken for a hang): appended
+    to gpurun_out/heartbeat.log when that directory exists (pytest captures fd 2 during a test)"""
+
+    def __init__(self, what):
+        import threading
+        self.what, self.t0, self.stop = what, time.time(), threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        d = os.path.join(REPO, "gpurun_out")
+        while not self.stop.wait(60):
+            line = "[configs] ... %s %.0fs\n" % (self.what, time.time() - self.t0)
+            if os.path.isdir(d):
+                with open(os.path.join(d, "heartbeat.log"), "a") as f:
+                    f.write(line)
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop.set()
+
+
 def _batch_and_check(request, gi, oi, strs, m, k, strategy, n_random):
     """Run the whole batch on the GPU; compare a random sample plus every tier >= 1 read."""
     import gwa
@@ -86,7 +111,8 @@ def _batch_and_check(request, gi, oi, strs, m, k, strategy, n_random):
     cfg = gwa.AlignmentConfig(k=k, strategy=strategy)
     t0 = time.time()
     b = gwa.Batch(gi, cfg, reads)
-    b.run()
+    with _Heartbeat("GPU batch"):
+        b.run()
     st = b.stats()
     c = b.read_counters()
     deep = np.nonzero(c[:, 12] >= 1)[0]
@@ -95,8 +121,9 @@ def _batch_and_check(request, gi, oi, strs, m, k, strategy, n_random):
     got, _ = b.results_select(samp)
     b.close()
     t1 = time.time()
-    exp = oi.align([reads[i] for i in samp], O.OrcConfig.default(k=k, strategy=gwa.STRATEGIES[strategy]),
-                   threads=_threads())
+    with _Heartbeat("oracle"):
+        exp = oi.align([reads[i] for i in samp], O.OrcConfig.default(k=k, strategy=gwa.STRATEGIES[strategy]),
+                       threads=_threads())
     _say(request, "%s k=%g m=%d: %d reads on the GPU (tiers %s, %.1fs), %d compared (%d from tiers >= 1) in %.1fs"
          % (strategy, k, m, n, list(st.tier_reads), t1 - t0, len(samp), len(deep), time.time() - t1))
     _compare(got, exp)
@@ -125,18 +152,20 @@ def test_c4_full_size_hg19r_indels_k5(hg19r_full, request):
 
 @pytest.mark.timeout(900)
 def test_c4_full_size_hg19r_indels_k5_sf(hg19r_full, request):
-    """C4 with -m sf on the full-size hg19-like genome, every read compared with the oracle.  The
-    reference's SuffixFilter loop has no search cap (S/SuffixFilter.java:257-290): on the full-size
-    repeat families (1M Alu-like copies) a few reads in a thousand queue over 200k states at once and
-    verify over 500k candidate positions (tools/diag_sf.py on these reads: 1.5M SFStates, 511k DP
-    verifications for the heaviest; the oracle needs 7 s for it).  The device holds them in the grown
-    last tier (gwa_batch_run) -- no read is refused -- but such a search runs on one lane
-    for minutes, so this test takes 2000 reads of the C4 stream (reads_codes, config 4; 245 need a tier >= 1,
-    2 the sixth), not 100k: minutes on the GPU, all 2000 compared byte for byte."""
+    """C4 with -m sf on the full-size hg19-like genome.  The reference's SuffixFilter loop has no
+    search cap (S/SuffixFilter.java:257-290): on the full-size repeat families (1M Alu-like copies) a
+    few reads in a thousand queue over 200k states at once and verify over 500k candidate positions
+    (tools/diag_sf.py: 1.6M SFStates, 511k DP verifications for the heaviest of 2000; the oracle needs
+    7 s for it on one core).  Such reads reach the grown last tier, run by the cooperative kernel
+    (search_kernels.h sf_search_kernel COOP: lane 0 searches, deferring its verifications; lanes 1-63
+    run them in passes of 63; a roll-back when a result would lower minMismatches) -- round 5 took
+    the 2000-read batch from 228 s to ~60 s on the GPU.  4000 reads of the C4 stream on the GPU;
+    3000 random + every tier >= 1 read compared byte for byte with the oracle (16 threads); both
+    times are printed."""
     codes, names, lengths, gi, oi = hg19r_full
-    strs = synth.to_strings(synth.reads_codes(codes, lengths, 2000, 150, 2, config_id=4, indels=True, max_edits=5))
-    st, deep = _batch_and_check(request, gi, oi, strs, 150, 5.0, "sf", 2000)
-    assert st.tier_reads[3] > 0 and len(deep) > 100
+    strs = synth.to_strings(synth.reads_codes(codes, lengths, 4000, 150, 2, config_id=4, indels=True, max_edits=5))
+    st, deep = _batch_and_check(request, gi, oi, strs, 150, 5.0, "sf", 3000)
+    assert st.tier_reads[3] > 0 and len(deep) > 200
 
 
 # ---- C3: reads sharded over processes, one index replica per process ----
