@@ -223,7 +223,7 @@ struct Caps {
   int32_t cand;  // SuffixFilter candidate set (sf_core.h); 0 on the BSF path
   int32_t sparse;  // > 1: only every sparse-th lane of a wavefront takes reads (deep tiers, bsf_search_kernel)
   int32_t sf;      // 1: the arena holds SfState<R> (sf_core.h), else DState<R>
-  int32_t spec;    // -m sf sparse last tier: speculative verification results (SfLane::SpecEntry, a power of two)
+  int32_t spec;    // -m sf sparse last tier: verification result table entries (SfLane::SpecEntry, a power of two)
 };
 // bytes of one arena slot: SfState<R> is 24 + 8 R bytes (static_assert in sf_core.h)
 template <int R>

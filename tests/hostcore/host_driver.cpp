@@ -91,7 +91,7 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         while (bc.cand < 2 * bc.hits && bc.cand < (1 << 22)) bc.cand <<= 1;
       }
       // HC_SF_COOP=1: -m sf through the cooperative kernel's algorithm (search_kernels.h sf_search_kernel
-      // COOP: speculative verification by 63 helper lanes sharing the slice) on every tier
+      // COOP: deferred verification, 63 helper lanes sharing the slice) on every tier
       const bool coop = strategy == 1 && getenv("HC_SF_COOP") && atoi(getenv("HC_SF_COOP")) != 0;
       if (coop) {
         sc.spec = 64;

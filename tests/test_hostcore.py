@@ -145,7 +145,7 @@ def test_sf_repetitive_genome(repetitive_genome, m, k, sub, chim):
 
 
 @pytest.mark.parametrize("case", ["indels150", "rep100", "rep50chim", "rep_rt2"])
-def test_sf_cooperative_speculation(random_genome, repetitive_genome, case, monkeypatch):
+def test_sf_cooperative_deferred_verification(random_genome, repetitive_genome, case, monkeypatch):
     """-m sf through the cooperative kernel's algorithm (search_kernels.h sf_search_kernel COOP, run
     by the GPU on the sparse last tier), here on every tier: the owner lane defers its verifications
     and goes on searching, 63 helper lanes run them in passes, the owner commits them in order and
