@@ -80,6 +80,27 @@ size_t cacheRound(size_t b) {
   const size_t step = std::max<size_t>(256, ((size_t)1 << e) / 8);
   return (b + step - 1) / step * step;
 }
+// give every idle cached block of the current device back to the driver (index close, allocation
+// failures): blocks idle in the cache are invisible to hipMemGetInfo
+void devCacheTrim() {
+  DevCache &c = devCache();
+  std::lock_guard<std::mutex> g(c.mu);
+  for (auto &kv : c.free) {
+    (void)hipFree(kv.second);
+    c.size.erase(kv.second);
+  }
+  c.free.clear();
+  c.cached = 0;
+}
+size_t devCacheIdle() {
+  DevCache &c = devCache();
+  std::lock_guard<std::mutex> g(c.mu);
+  return c.cached;
+}
+// Per device: reading the free memory and allocating the search scratch it sizes are one step, so
+// batches of several host threads (gwa_pipeline workers) cannot each size their scratch from the
+// same free memory (gwa_batch_run holds it from scratchBudget to the tier's last allocation).
+std::mutex g_allocMu[64];
 void *batchMalloc(size_t bytes) {
   DevCache &c = devCache();
   const size_t r = cacheRound(bytes);
@@ -96,13 +117,7 @@ void *batchMalloc(size_t bytes) {
   void *p = nullptr;
   if (hipMalloc(&p, r) != hipSuccess) {  // give the cached blocks back and try once more
     (void)hipGetLastError();
-    std::lock_guard<std::mutex> g(c.mu);
-    for (auto &kv : c.free) {
-      (void)hipFree(kv.second);
-      c.size.erase(kv.second);
-    }
-    c.free.clear();
-    c.cached = 0;
+    devCacheTrim();
     HIPCHK(hipMalloc(&p, r));
   }
   std::lock_guard<std::mutex> g(c.mu);
@@ -217,7 +232,22 @@ struct Scratch {
   void ensure(size_t need) {
     if (need <= bytes) return;
     release();
-    HIPCHK(hipMalloc(&p, need));
+    if (hipMalloc(&p, need) != hipSuccess) {
+      // memory held idle elsewhere in this process: the device cache's blocks and the index's
+      // idle scratch buffers (other batches' are in use) -- given back, then one more try
+      (void)hipGetLastError();
+      p = nullptr;
+      devCacheTrim();
+      {
+        std::lock_guard<std::mutex> g(ix->scratchMu);
+        for (auto &f : ix->scratchFree) {
+          (void)hipFree(f.first);
+          ix->scratchHeld -= f.second;
+        }
+        ix->scratchFree.clear();
+      }
+      HIPCHK(hipMalloc(&p, need));
+    }
     bytes = need;
     std::lock_guard<std::mutex> g(ix->scratchMu);
     ix->scratchHeld += need;
@@ -316,6 +346,7 @@ static void freeIndexDev(gwa_index *ix) {
   for (auto &f : ix->scratchFree) (void)hipFree(f.first);
   ix->scratchFree.clear();
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
+  devCacheTrim();  // (the device's idle batch buffers: no batch of a closed index reuses them)
 }
 
 namespace gwa {
@@ -954,10 +985,12 @@ static uint32_t tierValue(const char *var, int t, uint32_t def) {
 
 // Search scratch one batch's tiers may hold: half of what is free on the device plus the buffer the
 // batch already holds, at most 64 GiB (the index replica and the other batches keep the rest).
+// Idle blocks of the device cache count as free (Scratch::ensure gives them back when it needs
+// them).  Called under g_allocMu of the device, with the allocations it sizes.
 static uint64_t scratchBudget(size_t held) {
   size_t freeB = 0, totalB = 0;
   if (hipMemGetInfo(&freeB, &totalB) != hipSuccess) return 16ull << 30;
-  return std::min<uint64_t>(64ull << 30, ((uint64_t)freeB + held) / 2);
+  return std::min<uint64_t>(64ull << 30, ((uint64_t)freeB + held + devCacheIdle()) / 2);
 }
 
 // the batch's output slots + pool (gwa_layout.h OutSlots); pool counters at d_count[12..14]
@@ -1143,6 +1176,9 @@ int gwa_batch_run(gwa_batch_t *b) {
     };
     while (n > 0) {
       if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
+      // the budget and this tier's scratch / resume allocations as one step per device (released
+      // before the launch: the memory is allocated by then, so the next batch's budget sees it)
+      std::unique_lock<std::mutex> allocLock(g_allocMu[ix->device & 63]);
       const uint64_t budget = scratchBudget(scr.bytes);
       // Few reads left after the first tier: straight to the largest tier whose capacities give every
       // one of them a slice within the scratch budget.  A rerun restarts a search from its seeds, and
@@ -1225,6 +1261,7 @@ int gwa_batch_run(gwa_batch_t *b) {
         rb.inStride = resIn.stride;
         rb.inCap = resIn.cap;
       }
+      allocLock.unlock();
       HIPCHK(hipEventRecord(e1, s));
       const OutSlots os = outSlots(b);
 #ifdef GWA_PROF

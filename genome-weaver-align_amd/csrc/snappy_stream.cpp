@@ -37,11 +37,15 @@ void snappyBlock(const unsigned char *in, size_t n, std::string &out) {
   size_t p = 0;
   uint64_t ulen = 0;
   for (int shift = 0;; shift += 7) {
-    if (p >= n || shift > 35) throw std::runtime_error("corrupt snappy block (length)");
+    // (Snappy's length is a uint32: at most 5 varint bytes)
+    if (p >= n || shift > 28) throw std::runtime_error("corrupt snappy block (length)");
     const unsigned char b = in[p++];
     ulen |= (uint64_t)(b & 0x7F) << shift;
     if (!(b & 0x80)) break;
   }
+  // checked before the output is sized: no element expands more than 22x (a 3-byte copy of 64
+  // bytes), so a larger claimed length is corrupt, not a reason to allocate it
+  if (ulen > 0xFFFFFFFFull || ulen > 64 * (uint64_t)n + 64) throw std::runtime_error("corrupt snappy block (length)");
   const size_t base = out.size();
   out.resize(base + ulen);
   char *o = &out[0] + base;
@@ -113,6 +117,11 @@ void snappyJavaDecode(const unsigned char *in, size_t n, std::string &out) {
 SnapReader::SnapReader(const char *path) : path_(path) {
   f_ = fopen(path, "rb");
   if (!f_) throw std::runtime_error(std::string("cannot open ") + path);
+  if (fseeko(f_, 0, SEEK_END) == 0) {
+    const off_t e = ftello(f_);
+    fileSize_ = e > 0 ? (uint64_t)e : 0;
+  }
+  if (fseeko(f_, 0, SEEK_SET) != 0) throw std::runtime_error(std::string("cannot read ") + path);
   unsigned char h[16];
   const size_t got = fread(h, 1, 16, f_);
   if (got == 16 && memcmp(h, kMagic, 8) == 0) {
@@ -141,6 +150,8 @@ bool SnapReader::fill() {
   }
   if (g != 4) throw std::runtime_error(std::string("truncated snappy stream: ") + path_);
   const uint32_t c = be32(lb);
+  const off_t at = ftello(f_);
+  if (at < 0 || (uint64_t)at + c > fileSize_) throw std::runtime_error(std::string("truncated snappy stream: ") + path_);
   comp_.resize(c);
   if (c && fread(&comp_[0], 1, c, f_) != c) throw std::runtime_error(std::string("truncated snappy stream: ") + path_);
   buf_.clear();

@@ -26,6 +26,7 @@ class SnapReader {
   std::string path_, comp_, buf_;
   FILE *f_ = nullptr;
   size_t pos_ = 0;
+  uint64_t fileSize_ = 0;  // (a chunk length is checked against the bytes left before any allocation)
   bool stream_ = false, eof_ = false;
 };
 

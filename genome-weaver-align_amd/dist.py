@@ -68,7 +68,7 @@ def gather_sam_device(sam, dst=0):
     """Gather each rank's SAM text held in a uint8 tensor (on the GPU with the nccl backend = RCCL over
     xGMI, or on the CPU with gloo) to `dst`, concatenated in rank order = input order.  One all-gather
     of the lengths (8 bytes per rank), then every other rank sends its text once, point to point, into
-    its slice of the merged buffer on `dst`: each text crosses the fabric once and no rank but `dst`
+    its slice of the merged buffer on `dst`, all receives posted together (`batch_isend_irecv`): each text crosses the fabric once and no rank but `dst`
     holds more than its own (an all-gather of padded texts would move N x the data into every rank).
     Returns the merged uint8 tensor on `dst`, None on the other ranks; the tensor itself without
     torch.distributed."""
@@ -84,14 +84,20 @@ def gather_sam_device(sam, dst=0):
     lens = [int(x.item()) for x in lens]
     if me != dst:
         if lens[me]:
-            td.send(sam, dst)
+            for req in td.batch_isend_irecv([td.P2POp(td.isend, sam, dst)]):
+                req.wait()
         return None
     out = torch.empty(sum(lens), dtype=torch.uint8, device=sam.device)
-    off = 0
+    # every receive posted at once (one batch): under RCCL the texts of up to 7 peers arrive over
+    # their own xGMI links concurrently instead of one link at a time
+    ops, off = [], 0
     for r, ln in enumerate(lens):
         if r == dst:
             out[off:off + ln].copy_(sam)
         elif ln:
-            td.recv(out[off:off + ln], src=r)
+            ops.append(td.P2POp(td.irecv, out[off:off + ln], r))
         off += ln
+    if ops:
+        for req in td.batch_isend_irecv(ops):
+            req.wait()
     return out

@@ -107,12 +107,16 @@ static int runAll(HC *x, int strategy, const SearchConfig &cfg, const StairTable
         const int hcap = sc.path / 2;
         static std::vector<uint8_t> hchunk;
         static std::vector<uint16_t> hcig;
-        hchunk.assign((size_t)64 * (ilvBytes(sc) + 64), 0);
+        // (each helper's interleaved block 64-B aligned, as a wavefront's block is on the GPU: the
+        // DP history is read and written as 16-B {vp, vn} pairs)
+        const size_t hstride = (ilvBytes(sc) + 64 + 63) & ~(size_t)63;
+        hchunk.assign((size_t)64 * hstride + 64, 0);
+        uint8_t *hbase = (uint8_t *)(((uintptr_t)hchunk.data() + 63) & ~(uintptr_t)63);
         hcig.assign((size_t)64 * hcap, 0);
         std::vector<CL> ln;
         ln.reserve(64);
         for (int h = 0; h < 64; ++h) {
-          LaneMem<R> Lh = laneMem<R>(scratch.data(), hchunk.data() + (size_t)h * (ilvBytes(sc) + 64), 0, 1, sc);
+          LaneMem<R> Lh = laneMem<R>(scratch.data(), hbase + (size_t)h * hstride, 0, 1, sc);
           ln.emplace_back(x->v, cfg, st, h == 0 ? L : Lh, sc);
           ln[h].chrRank = rk.data();
           ln[h].initRead(codes.data(), (int)mlen);

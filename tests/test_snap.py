@@ -49,6 +49,16 @@ def test_corrupt_streams_fail():
         gwa.snappy_decompress(bare)
     with pytest.raises(gwa.GwaError):
         gwa.snappy_decompress(bytes([0x80]))  # unterminated length varint
+    # lengths that would size terabytes of output before any element is checked: a 6-byte varint
+    # (Snappy's length is a uint32) and a 5-byte one far beyond what 10 input bytes can expand to
+    with pytest.raises(gwa.GwaError):
+        gwa.snappy_decompress(bytes([0xFF] * 5 + [0x7F, 0, 0, 0, 0]))
+    with pytest.raises(gwa.GwaError):
+        gwa.snappy_decompress(bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x0F, 0, 0, 0, 0, 0]))
+    # a stream chunk claiming more bytes than the data holds
+    hdr = data[:16]
+    with pytest.raises(gwa.GwaError):
+        gwa.snappy_decompress(hdr + bytes([0x7F, 0xFF, 0xFF, 0xFF, 1, 0]))
 
 
 def test_cli_reads_of_snap_equals_plain(tmp_path):
@@ -87,3 +97,18 @@ def test_pipeline_snap_file_matches_oracle(tmp_path):
         outs.append(out.getvalue())
     oi = O.Index.from_fasta(ref.read_text())
     assert outs[0] == outs[1] == oi.sam_header() + oi.align(reads, O.OrcConfig.default(k=2.0))
+
+
+@pytest.mark.gpu
+def test_pipeline_snap_chunk_longer_than_file_fails(tmp_path):
+    # the streaming reader (SnapReader, the pipeline's IO thread) checks a chunk's length against the
+    # bytes left in the file before sizing its buffer: a clean error, not a 2 GiB allocation
+    codes, names, lengths = snap_reads.genome()
+    import synth
+    ref = tmp_path / "ref.fa"
+    ref.write_text(synth.fasta_text(codes, names, lengths))
+    bad = tmp_path / "bad.fq.snap"
+    bad.write_bytes(_read("reads_c1.fq.snap")[:16] + bytes([0x7F, 0xFF, 0xFF, 0xFF]) + b"\x01\x00")
+    ns = gwa_cli.build_parser().parse_args(["align", "-r", str(ref), "-k", "2", "--batch", "64", str(bad)])
+    with pytest.raises(gwa.GwaError, match="snappy"):
+        gwa_cli.align(ns, out=io.StringIO())
