@@ -17,6 +17,7 @@
 // Also here: the batch statistics as a device reduction over the per-read output headers.
 #include <hip/hip_runtime.h>
 
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include <cstdlib>
@@ -369,6 +370,47 @@ void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipSt
   const uint32_t g = (n + 255) / 256;
   hipLaunchKernelGGL(statsKernel, dim3(g > 2048 ? 2048 : g), dim3(256), 0, s, oh, n, acc);
   FCHK(hipGetLastError());
+}
+
+// ---- the search list in quick-scan order (experiment, GWA_SEARCH_SORT) ----
+// Key of a searched read from its quick-scan result (ScanRes: each strand's numMismatches and
+// longest-match start, the seeds of S/BidirectionalSuffixFilter.java:318-341).  "lo" is the strand
+// with fewer mismatches (forward on a tie).  A stable radix sort keeps input order inside a key.
+__global__ void searchKeyKernel(const uint32_t *list, uint32_t n, const ScanRes *sres, int mode, uint32_t *keys) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ScanRes r = sres[list[i]];
+  const bool f = r.nmF <= r.nmR;
+  const uint32_t lo = (uint32_t)(f ? r.nmF : r.nmR) & 15, hi = (uint32_t)(f ? r.nmR : r.nmF) & 15;
+  const uint32_t lmLo = (uint32_t)(f ? r.lmF : r.lmR) & 511, lmHi = (uint32_t)(f ? r.lmR : r.lmF) & 511;
+  const uint32_t pat = lo << 4 | hi;
+  uint32_t k;
+  switch (mode) {
+    case 1: k = pat; break;
+    case 2: k = pat << 9 | lmLo >> 2; break;
+    case 3: k = ((((uint32_t)r.nmF & 15) << 4 | ((uint32_t)r.nmR & 15)) << 9 | ((uint32_t)r.lmF & 511) >> 2) << 9 |
+                ((uint32_t)r.lmR & 511) >> 2; break;
+    case 4: k = (pat << 9 | lmLo) << 9 | lmHi >> 2; break;
+    case 5: k = (lmLo >> 2) << 8 | pat; break;
+    case 7: k = list[i]; break;  // input order (a deep tier's list)
+    default: k = pat << 9 | lmLo >> 3; break;
+  }
+  keys[i] = k;
+}
+
+size_t sortSearchListTmpBytes(uint32_t n) {
+  size_t b = 0;
+  FCHK(rocprim::radix_sort_pairs(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                 (uint32_t *)nullptr, (size_t)n, 0, 32, (hipStream_t)0));
+  return b;
+}
+
+void launchSortSearchList(const uint32_t *listIn, uint32_t *listOut, uint32_t *keysIn, uint32_t *keysOut, uint32_t n,
+                          const ScanRes *sres, int mode, void *tmp, size_t tmpBytes, hipStream_t s) {
+  hipLaunchKernelGGL(searchKeyKernel, dim3((n + 255) / 256), dim3(256), 0, s, listIn, n, sres, mode, keysIn);
+  FCHK(hipGetLastError());
+  size_t b = tmpBytes;
+  FCHK(rocprim::radix_sort_pairs(tmp, b, keysIn, keysOut, listIn, listOut, (size_t)n, 0, mode == 7 ? 32 : 26, s));
 }
 
 }  // namespace gwa

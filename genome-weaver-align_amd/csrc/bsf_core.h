@@ -130,35 +130,6 @@ GWA_HD void loadBlock(const OccBlock *occ, uint64_t b, Block &o) {
 #endif
 }
 
-// Quad-per-read load (the quick-scan kernel's QUAD layout: the four lanes of a quad run the same read
-// in lock step): lane j of the quad loads the j-th 16 B of the block and DPP quad broadcasts give every
-// lane all four parts -- one 64-B request per block instead of four 16-B requests from each lane
-GWA_HD void loadBlockQuad(const OccBlock *occ, uint64_t b, Block &o) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(occ + b) + (__lane_id() & 3));
-  uint32_t w[16];
-#define GWA_QB(j)                                                                    \
-  w[4 * (j) + 0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.x, (j) * 0x55, 0xF, 0xF, false); \
-  w[4 * (j) + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.y, (j) * 0x55, 0xF, 0xF, false); \
-  w[4 * (j) + 2] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.z, (j) * 0x55, 0xF, 0xF, false); \
-  w[4 * (j) + 3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.w, (j) * 0x55, 0xF, 0xF, false);
-  GWA_QB(0) GWA_QB(1) GWA_QB(2) GWA_QB(3)
-#undef GWA_QB
-  o.cnt[0] = w[0]; o.cnt[1] = w[1]; o.cnt[2] = w[2]; o.cnt[3] = w[3];
-  o.lo0 = ((uint64_t)w[5] << 32) | w[4]; o.lo1 = ((uint64_t)w[7] << 32) | w[6];
-  o.hi0 = ((uint64_t)w[9] << 32) | w[8]; o.hi1 = ((uint64_t)w[11] << 32) | w[10];
-  o.n0 = ((uint64_t)w[13] << 32) | w[12]; o.n1 = ((uint64_t)w[15] << 32) | w[14];
-#else
-  loadBlock(occ, b, o);
-#endif
-}
-template <bool QUAD>
-GWA_HD void loadBlockQ(const OccBlock *occ, uint64_t b, Block &o) {
-  if (QUAD) loadBlockQuad(occ, b, o);
-  else loadBlock(occ, b, o);
-}
-
 // counts of A,C,G,T,N in bwt[0, i) where i lies in block B (i>>7 == block index)
 GWA_HD void rankAll(const Block &B, uint64_t i, uint64_t out[5]) {
   const uint32_t r = (uint32_t)(i & 127);
@@ -1200,7 +1171,6 @@ struct BsfLane {
     return j < L ? j : L;
   }
 
-  template <bool QUAD = false>
   GWA_HD Scan quickScan(int strand) {
     const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
     const uint64_t N = ix.N;
@@ -1258,11 +1228,11 @@ struct BsfLane {
         // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
         // one 64-B block when lb and ub share a 128-position window
         Block B;
-        loadBlockQ<QUAD>(ix.occ[fm], lb >> 7, B);
+        loadBlock(ix.occ[fm], lb >> 7, B);
         ++blocks;
         nlb = ix.C[ch] + rankOne(B, lb, ch);
         if ((ub >> 7) != (lb >> 7)) {
-          loadBlockQ<QUAD>(ix.occ[fm], ub >> 7, B);
+          loadBlock(ix.occ[fm], ub >> 7, B);
           ++blocks;
         }
         nub = ix.C[ch] + rankOne(B, ub, ch);
@@ -2135,9 +2105,6 @@ struct BsfLane {
   // ---- AlignmentProcess.align_internal (:278-477), split at the quick scan ----
   // Phase 1 (fm_quickscan kernel): N check, FMQuickScan on both strands, exact hits.
   // Returns 1 when the read needs the best-first search; otherwise the result is final.
-  // QUAD: the quick-scan kernel's quad-per-read layout (loadBlockQuad; the quad's lanes are converged
-  // and write the same values)
-  template <bool QUAD = false>
   GWA_HD int quickPhase(ScanRes *sr, OutHeader *oh, const OutSlots &os, uint32_t rd_) {
     oh->fmSearches = 0;
     oh->states = 0;
@@ -2153,9 +2120,9 @@ struct BsfLane {
       const int countN = loadWords(pw0, pw1);
       if (countN > k) { finishQuick(oh); return 0; }
     }
-    Scan sF = quickScan<QUAD>(0);
+    Scan sF = quickScan(0);
     if (sF.numMismatches == 0) { reportExact(sF, 0, oh, os, rd_); return 0; }
-    Scan sR = quickScan<QUAD>(1);
+    Scan sR = quickScan(1);
     if (sR.numMismatches == 0) { reportExact(sR, 1, oh, os, rd_); return 0; }
     if (k == 0) { finishQuick(oh); return 0; }
     sr->nmF = sF.numMismatches; sr->lmF = sF.lmStart;

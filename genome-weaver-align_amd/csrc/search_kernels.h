@@ -26,15 +26,13 @@ __device__ __forceinline__ uint32_t waveAppend(bool need, uint32_t value, uint32
   return pos;
 }
 
-// QUAD: four lanes per read (a quad), in lock step on the same read; each Occ block is loaded as one
-// 64-B request split over the quad (loadBlockQuad).  Otherwise lane r scans read r.
-template <int QW, bool QUAD>
+template <int QW>
 __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres,
                                                            OutHeader *oh, OutSlots os,
                                                            uint32_t *searchList, uint32_t *searchCount,
                                                            uint32_t *trace, int traceRead) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t r = QUAD ? t >> 2 : t;
+  // lane r scans read r
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   bool need = false;
   if (r < reads.n) {
     const uint32_t o = reads.off[r];
@@ -48,13 +46,13 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
       LaneMem<4> L{};
       Caps caps{};
       BsfLane<4, QW> lane(ix, cfg, st, L, caps);
-      if (trace && (int)r == traceRead && (!QUAD || (t & 3) == 0)) { lane.trace = trace + 1; lane.traceCap = 65536; }
+      if (trace && (int)r == traceRead) { lane.trace = trace + 1; lane.traceCap = 65536; }
       lane.initRead(reads.codes + o, m);
-      need = lane.template quickPhase<QUAD>(sres + r, h, os, r) != 0;
+      need = lane.quickPhase(sres + r, h, os, r) != 0;
       if (lane.trace) trace[0] = (uint32_t)lane.traceN;
     }
   }
-  waveAppend(need && (!QUAD || (t & 3) == 0), r, searchList, searchCount);
+  waveAppend(need, r, searchList, searchCount);
 }
 
 #ifndef GWA_SEARCH_WAVES
@@ -423,14 +421,8 @@ template <int QW>
 void launchQuickscanT(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
                       int traceRead) {
-  // GWA_QUICK_QUAD=0: one lane per read (A/B runs)
-  const bool quad = !(getenv("GWA_QUICK_QUAD") && atoi(getenv("GWA_QUICK_QUAD")) == 0);
-  if (quad)
-    hipLaunchKernelGGL((fm_quickscan_kernel<QW, true>), dim3(((uint64_t)reads.n * 4 + 255) / 256), dim3(256), 0, s, ix, cfg,
-                       reads, sres, oh, os, searchList, searchCount, trace, traceRead);
-  else
-    hipLaunchKernelGGL((fm_quickscan_kernel<QW, false>), dim3((reads.n + 255) / 256), dim3(256), 0, s, ix, cfg, reads, sres,
-                       oh, os, searchList, searchCount, trace, traceRead);
+  hipLaunchKernelGGL(fm_quickscan_kernel<QW>, dim3((reads.n + 255) / 256), dim3(256), 0, s, ix, cfg, reads, sres, oh, os,
+                     searchList, searchCount, trace, traceRead);
 }
 
 // one (QW, R) instance set per translation unit (search_inst.hip, built once per pair by the

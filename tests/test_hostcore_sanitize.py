@@ -164,9 +164,10 @@ def test_sanitized_hostcore_matches_oracle(san, case, random_genome, repetitive_
     assert got == exp
 
 
-# 257..512 bp reads (QW = 16) at the k's of test_hostcore.py::LONG_CASES, including the -m sf 400 bp
-# k = 0.06 case whose reads the GPU lost in round 5 (gpurun_out/j13/long_coop.log), read by read:
-# the reference throws on some (m, k) filters, and the program must fail exactly where it does
+# 257..512 bp reads (QW = 16) at the k's of test_hostcore.py::LONG_CASES, on the same 60 reads per case
+# as tests/test_gpu_parity.py::test_long_reads_on_gpu -- including the -m sf 400 bp k = 0.06 case whose
+# reads r19, r23 and r39 the GPU lost in round 5 (gpurun_out/j13/long_coop.log): the reads the oracle
+# aligns as one batch (its SAM), and each read the reference throws on alone (the program must fail)
 LONG = [(0, 300, 5.0), (0, 400, 2.0), (0, 512, 31.0), (1, 400, 0.06), (1, 400, 5.0), (1, 480, 5.0), (1, 333, 2.0)]
 
 
@@ -174,9 +175,14 @@ LONG = [(0, 300, 5.0), (0, 400, 2.0), (0, 512, 31.0), (1, 400, 0.06), (1, 400, 5
 @pytest.mark.parametrize("strategy,m,k", LONG)
 def test_sanitized_long_reads(san, strategy, m, k):
     binary = _binary(san)
-    genome = synth.genome([("c1", 150000), ("c2", 50000)], config_id=3)
-    seqs, rn = synth.reads(genome[0], genome[2], 12, m, 3, config_id=4 + m)
+    genome = synth.genome([("c1", 300000), ("c2", 200000)], 1)  # (test_gpu_parity.py random_pair)
+    seqs, rn = synth.reads(genome[0], genome[2], 60, m, 3, config_id=4 + m)
     strs = synth.to_strings(seqs)
+    good, bad = [], []
     for i, s in enumerate(strs):
-        r = [("r%d" % i, s, "I" * m)]
-        assert _run(binary, genome, r, k, strategy=strategy) == _expect(genome, r, k, strategy=strategy), (m, k, i)
+        r = ("r%d" % i, s, "I" * m)
+        (good if _expect(genome, [r], k, strategy=strategy) is not None else bad).append(r)
+    assert good
+    assert _run(binary, genome, good, k, strategy=strategy) == _expect(genome, good, k, strategy=strategy), (m, k)
+    for r in bad[:4]:
+        assert _run(binary, genome, [r], k, strategy=strategy) is None, (m, k, r[0])

@@ -10,6 +10,6 @@ rm -rf $D && mkdir -p $D && cp -r $REPO/genome-weaver-align_amd/csrc $REPO/genom
 mkdir -p $D/../include_$NAME && cp $REPO/include/gwa.h $D/../include_$NAME/
 sed -i "s#../../include/gwa.h#$REPO/include/gwa.h#" $D/csrc/*.cpp $D/csrc/*.h $D/csrc/*.hip 2>/dev/null || true
 (cd $D/csrc && python3 $PATCH)
-make -s -j8 -C $D HDR="$(echo $D/csrc/*.h) $REPO/include/gwa.h" libgwa.so
+make -s -j${VJ:-8} -C $D HDR="$(echo $D/csrc/*.h) $REPO/include/gwa.h" libgwa.so
 cp $D/libgwa.so $REPO/genome-weaver-align_amd/libgwa_$NAME.so
 echo built $REPO/genome-weaver-align_amd/libgwa_$NAME.so
