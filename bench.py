@@ -301,22 +301,37 @@ def shard_processes_leg(np, synth, codes, names, lengths, d, fq, one_sam, n, han
     cli = os.path.join(REPO, "genome-weaver-align_amd", "gwa_cli.py")
     per = max(1, handles // nproc)
     outs, ps = [], []
+    sync = os.path.join(d, "sync")
+    os.makedirs(sync, exist_ok=True)
     t0 = time.perf_counter()
     for r in range(nproc):
         o = os.path.join(d, "shard%d.sam" % r)
         outs.append(o)
         with open(o, "wb") as fo:
             ps.append(subprocess.Popen([sys.executable, cli, "align", "-r", ref, "-k", "0", "--devices", ",".join(["0"] * per),
-                                        "--workers", "3", "--timing", "--warm-passes", "2", "--shard", "%d/%d" % (r, nproc), fq],
+                                        "--workers", "3", "--timing", "--warm-passes", "2", "--sync", "%s:%d" % (sync, nproc),
+                                        "--shard", "%d/%d" % (r, nproc), fq],
                                        stdout=fo, stderr=subprocess.PIPE, text=True))
     errs = [p.communicate()[1] for p in ps]
     wall = time.perf_counter() - t0
-    align_s = []
+    align_s, spans, stages = [], [], []
     for p, e in zip(ps, errs):
         if p.returncode != 0:
             return {"error": "shard process exited %d: %s" % (p.returncode, e[-400:])}
         line = [x for x in e.splitlines() if "align (read file -> SAM" in x][-1]
         align_s.append(float(line.split("index load excluded) ")[1].split("s")[0]))
+        mono = [x for x in e.splitlines() if "timed pass monotonic_ns" in x][-1].split()
+        spans.append((int(mono[-2]), int(mono[-1])))
+        # the process's own stage seconds (gwa_cli --timing: pipeline wall, read, frame; summed over its workers:
+        # parse, set-up, kernels, SAM format + D2H, write, order wait)
+        pl = [x for x in e.splitlines() if x.startswith("[gwa] pipeline ")]
+        if pl:
+            import re
+            v = [float(x) for x in re.findall(r"([0-9]+\.[0-9]+)s", pl[-1])]
+            stages.append(dict(zip(["wall", "read", "frame", "parse", "set_up", "sam_format_d2h", "write", "order_wait"],
+                                   v[:3] + v[3:5] + v[-3:])))
+    union_s = (max(b for _, b in spans) - min(a for a, _ in spans)) / 1e9
+    overlap_s = max(0.0, (min(b for _, b in spans) - max(a for a, _ in spans)) / 1e9)
 
     def digest(paths):
         h = hashlib.sha256()
@@ -334,10 +349,12 @@ def shard_processes_leg(np, synth, codes, names, lengths, d, fq, one_sam, n, han
     same = digest([os.path.join(d, "shard0.body")] + outs[1:]) == digest([one_sam])
     for x in outs + [os.path.join(d, "shard0.body"), ref]:
         os.remove(x)
-    out = {"processes": nproc, "handles_per_process": per, "reads_per_s": n / max(align_s), "align_s": align_s,
+    out = {"processes": nproc, "handles_per_process": per, "reads_per_s": n / union_s, "align_s": align_s,
+           "timed_union_s": union_s, "timed_overlap_s": overlap_s, "stages_s": stages,
            "wall_s_incl_start_and_index": wall, "concatenation_identical_to_one_process": same,
            "note": "gwa align --shard r/%d in %d processes on one GPU, each writing its own SAM shard; warm second pass "
-                   "(--warm-passes 2), index load excluded" % (nproc, nproc)}
+                   "(--warm-passes 2), started together (--sync), index load excluded; reads_per_s = all reads over the "
+                   "union of the timed passes (CLOCK_MONOTONIC)" % (nproc, nproc)}
     log("host ceiling, %d processes: %.1f M reads/s (align %s s), shards concatenated identical: %s"
         % (nproc, out["reads_per_s"] / 1e6, ["%.2f" % x for x in align_s], same))
     return out

@@ -372,30 +372,29 @@ void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipSt
   FCHK(hipGetLastError());
 }
 
-// ---- the search list in quick-scan order (experiment, GWA_SEARCH_SORT) ----
-// Key of a searched read from its quick-scan result (ScanRes: each strand's numMismatches and
-// longest-match start, the seeds of S/BidirectionalSuffixFilter.java:318-341).  "lo" is the strand
-// with fewer mismatches (forward on a tie).  A stable radix sort keeps input order inside a key.
-__global__ void searchKeyKernel(const uint32_t *list, uint32_t n, const ScanRes *sres, int mode, uint32_t *keys) {
+// ---- the first tier's search list in quick-scan order (gwa_batch_run) ----
+// The searched reads' order does not change any result (each lane runs its own reads to the end), but
+// it decides which reads share a wavefront.  A read's best-first search starts from seeds given by its
+// quick scan (each strand's numMismatches and longest-match start, S/BidirectionalSuffixFilter.java:
+// 318-341), so reads with the same seeds walk trees of a similar shape: they reach their reports and
+// finish at similar times and the wavefront's lanes stay busy together.  Key (byKey): the
+// longest-match start of the strand with fewer mismatches (4-base buckets), then the two strands'
+// mismatch counts (fewer, more).  !byKey: the read index (a deep tier's list back in input order).
+// A stable radix sort keeps input order inside a key.  Measured per 10M C2 reads (search ms, hg19 /
+// hg19r): unsorted 89.0 / 158.5, this key 77.2 / 142.1; DESIGN.md §4 has the other keys tried.
+__global__ void searchKeyKernel(const uint32_t *list, uint32_t n, const ScanRes *sres, int byKey, uint32_t *keys) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const ScanRes r = sres[list[i]];
-  const bool f = r.nmF <= r.nmR;
-  const uint32_t lo = (uint32_t)(f ? r.nmF : r.nmR) & 15, hi = (uint32_t)(f ? r.nmR : r.nmF) & 15;
-  const uint32_t lmLo = (uint32_t)(f ? r.lmF : r.lmR) & 511, lmHi = (uint32_t)(f ? r.lmR : r.lmF) & 511;
-  const uint32_t pat = lo << 4 | hi;
-  uint32_t k;
-  switch (mode) {
-    case 1: k = pat; break;
-    case 2: k = pat << 9 | lmLo >> 2; break;
-    case 3: k = ((((uint32_t)r.nmF & 15) << 4 | ((uint32_t)r.nmR & 15)) << 9 | ((uint32_t)r.lmF & 511) >> 2) << 9 |
-                ((uint32_t)r.lmR & 511) >> 2; break;
-    case 4: k = (pat << 9 | lmLo) << 9 | lmHi >> 2; break;
-    case 5: k = (lmLo >> 2) << 8 | pat; break;
-    case 7: k = list[i]; break;  // input order (a deep tier's list)
-    default: k = pat << 9 | lmLo >> 3; break;
+  const uint32_t r = list[i];
+  if (!byKey) {
+    keys[i] = r;
+    return;
   }
-  keys[i] = k;
+  const ScanRes q = sres[r];
+  const bool f = q.nmF <= q.nmR;
+  const uint32_t lo = (uint32_t)(f ? q.nmF : q.nmR) & 15, hi = (uint32_t)(f ? q.nmR : q.nmF) & 15;
+  const uint32_t lm = (uint32_t)(f ? q.lmF : q.lmR) & 511;
+  keys[i] = (lm >> 2) << 8 | lo << 4 | hi;
 }
 
 size_t sortSearchListTmpBytes(uint32_t n) {
@@ -406,11 +405,11 @@ size_t sortSearchListTmpBytes(uint32_t n) {
 }
 
 void launchSortSearchList(const uint32_t *listIn, uint32_t *listOut, uint32_t *keysIn, uint32_t *keysOut, uint32_t n,
-                          const ScanRes *sres, int mode, void *tmp, size_t tmpBytes, hipStream_t s) {
-  hipLaunchKernelGGL(searchKeyKernel, dim3((n + 255) / 256), dim3(256), 0, s, listIn, n, sres, mode, keysIn);
+                          const ScanRes *sres, bool byKey, void *tmp, size_t tmpBytes, hipStream_t s) {
+  hipLaunchKernelGGL(searchKeyKernel, dim3((n + 255) / 256), dim3(256), 0, s, listIn, n, sres, byKey ? 1 : 0, keysIn);
   FCHK(hipGetLastError());
   size_t b = tmpBytes;
-  FCHK(rocprim::radix_sort_pairs(tmp, b, keysIn, keysOut, listIn, listOut, (size_t)n, 0, mode == 7 ? 32 : 26, s));
+  FCHK(rocprim::radix_sort_pairs(tmp, b, keysIn, keysOut, listIn, listOut, (size_t)n, 0, byKey ? 15 : 32, s));
 }
 
 }  // namespace gwa

@@ -1089,13 +1089,12 @@ int gwa_batch_run(gwa_batch_t *b) {
     double searchMs = 0;
     int cur = 0;
     uint32_t n = nSearch;
-    // GWA_SEARCH_SORT=1|2 (experiment): the first tier takes the searched reads in quick-scan key order
-    // (launchSortSearchList) instead of input order; the results do not depend on the order
-    int firstSort = 0;
-    if (const char *ss = getenv("GWA_SEARCH_SORT")) {
-      const int mode = atoi(ss);
-      if (!sf && mode > 0 && n > 1) firstSort = mode;
-    }
+    // The first tier takes the searched reads in quick-scan key order (launchSortSearchList: reads
+    // with the same seeds share wavefronts), and the second tier takes the first tier's overflows in
+    // input order (in the first tier's completion order, i.e. key order, the heavy reads of one key
+    // would crowd the same wavefronts: C4 tier 1 158 ms against 112 ms).  -m sf searches every read in
+    // input order.  GWA_SEARCH_SORT=0: no sorting (A/B runs).
+    const bool sortLists = !sf && !(getenv("GWA_SEARCH_SORT") && atoi(getenv("GWA_SEARCH_SORT")) == 0);
     const int m = std::max(b->maxM, 1);
     int t = 0, regrow = 0, launches = 0;
     // Reads that overflow the last tier rerun on it with the exceeded capacities doubled (OV_* bits
@@ -1181,13 +1180,13 @@ int gwa_batch_run(gwa_batch_t *b) {
       caps.dpSlice = tb == 0 ? 1 : 0;  // the first tier's DP keeps the diagonal slice (bsf_core.h)
       return caps;
     };
-    // the search-list sort as one helper (tier 0: by quick-scan key; the second tier: see below)
-    auto sortList = [&](int mode) {
+    // the search-list sort (tier 0: by quick-scan key; the second tier: input order)
+    auto sortList = [&](bool byKey) {
       const size_t tb = sortSearchListTmpBytes(n);
       uint32_t *keys = bAlloc<uint32_t>(2 * (size_t)n);
       void *tmp = batchMalloc(std::max<size_t>(tb, 64));
       HIPCHK(hipEventRecord(e1, s));
-      launchSortSearchList(b->d_list[cur], b->d_list[cur ^ 1], keys, keys + n, n, b->d_sres, mode, tmp, tb, s);
+      launchSortSearchList(b->d_list[cur], b->d_list[cur ^ 1], keys, keys + n, n, b->d_sres, byKey, tmp, tb, s);
       HIPCHK(hipEventRecord(e2, s));
       HIPCHK(hipStreamSynchronize(s));
       float ms = 0;
@@ -1199,11 +1198,9 @@ int gwa_batch_run(gwa_batch_t *b) {
     };
     while (n > 0) {
       if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
-      // GWA_SORT_T1 (experiment): the second tier's list (the first tier's overflows, no resume
-      // records) in input order (7) or by quick-scan key (1-6) instead of the first tier's completion order
-      if (t == 1 && !sf && n > 1 && resIn.cap == 0 && getenv("GWA_SORT_T1") && atoi(getenv("GWA_SORT_T1")) > 0)
-        sortList(atoi(getenv("GWA_SORT_T1")));
-      if (t == 0 && firstSort > 0) sortList(firstSort);
+      // (the second tier's input has no resume records -- the first tier does not suspend -- so its
+      // list may be reordered; deeper tiers find their records by list position)
+      if (sortLists && n > 1 && (t == 0 || (t == 1 && resIn.cap == 0))) sortList(t == 0);
       // the budget and this tier's scratch / resume allocations as one step per device (released
       // before the launch: the memory is allocated by then, so the next batch's budget sees it)
       std::unique_lock<std::mutex> allocLock(g_allocMu[ix->device & 63]);

@@ -57,7 +57,7 @@ void launchSamFormat(const SamText &t, const OutHeader *oh, const OutHit *hits, 
 size_t samScanTempBytes(uint32_t n);
 size_t sortSearchListTmpBytes(uint32_t n);
 void launchSortSearchList(const uint32_t *listIn, uint32_t *listOut, uint32_t *keysIn, uint32_t *keysOut, uint32_t n,
-                          const ScanRes *sres, int mode, void *tmp, size_t tmpBytes, hipStream_t s);
+                          const ScanRes *sres, bool byKey, void *tmp, size_t tmpBytes, hipStream_t s);
 void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipStream_t s);
 size_t laneBytesFor(int R, const Caps &c);  // per-lane slice
 size_t ilvBytesFor(const Caps &c);          // per-lane share of the interleaved DP block

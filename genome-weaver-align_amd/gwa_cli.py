@@ -139,11 +139,27 @@ def build_parser():
     a.add_argument("--insert-max", type=int, default=390,
                    help="paired-end: largest template length of a proper pair (mate rescue needs max - min + read "
                         "length + 2k <= 320 bases; wider ranges pair without rescue)")
+    a.add_argument("--sync", default=None, metavar="DIR:N",
+                   help="timing runs of N processes (--shard): after the warm passes, wait until all N have written a "
+                        "ready file into DIR, so their timed passes run at the same time; --timing then also prints "
+                        "the timed pass's CLOCK_MONOTONIC start and end")
     a.add_argument("--shard", default=None, metavar="R/N",
                    help="one process per GPU: align contiguous shard R of N of the (plain) read file; the SAM "
                         "header is written by shard 0 only, so the shards' outputs concatenated in order are "
                         "the one-process SAM")
     return ap
+
+
+def sync_wait(spec, timeout=600.0):
+    """--sync DIR:N: write DIR/ready.<pid>, then wait until N ready files exist"""
+    d, n = spec.rsplit(":", 1)
+    n = int(n)
+    open(os.path.join(d, "ready.%d" % os.getpid()), "w").close()
+    t0 = time.monotonic()
+    while sum(1 for x in os.listdir(d) if x.startswith("ready.")) < n:
+        if time.monotonic() - t0 > timeout:
+            raise gwa.GwaError("--sync %s: the other processes did not arrive" % spec)
+        time.sleep(0.0005)
 
 
 def shard_of(ns):
@@ -240,8 +256,11 @@ def align(ns, out=sys.stdout):
                 for _ in range(max(0, ns.warm_passes - 1)):
                     with open(os.devnull, "wb") as dn:
                         pipe.align_file(ns.readFiles[0], dn.fileno(), shard=shard)
-                if ns.warm_passes > 1:
+                if ns.sync:
+                    sync_wait(ns.sync)
+                if ns.warm_passes > 1 or ns.sync:
                     t1, t_open = time.perf_counter(), 0.0
+                mono0 = time.monotonic_ns()
                 if ns.silent:
                     with open(os.devnull, "wb") as dn:
                         n = pipe.align_file(ns.readFiles[0], dn.fileno(), shard=shard)
@@ -266,6 +285,8 @@ def align(ns, out=sys.stdout):
                             out.write(tf.read().decode())
             finally:
                 t2 = time.perf_counter()  # (the SAM is written; unpinning the buffers is teardown)
+                if ns.timing and ns.sync:
+                    print("[gwa] timed pass monotonic_ns %d %d" % (mono0, time.monotonic_ns()), file=sys.stderr)
                 pipe.close()
         if ns.query is not None or len(ns.readFiles) == 2:
             t2 = time.perf_counter()
