@@ -395,6 +395,7 @@ __global__ void searchKeyKernel(const uint32_t *list, uint32_t n, const ScanRes 
   const uint32_t lo = (uint32_t)(f ? q.nmF : q.nmR) & 15, hi = (uint32_t)(f ? q.nmR : q.nmF) & 15;
   const uint32_t lm = (uint32_t)(f ? q.lmF : q.lmR) & 511;
   keys[i] = (lm >> 2) << 8 | lo << 4 | hi;
+  if (byKey == 2) keys[i] = keys[i] << 7 | (((uint32_t)(f ? q.feF : q.feR) & 511) >> 2);
 }
 
 size_t sortSearchListTmpBytes(uint32_t n) {
@@ -406,10 +407,11 @@ size_t sortSearchListTmpBytes(uint32_t n) {
 
 void launchSortSearchList(const uint32_t *listIn, uint32_t *listOut, uint32_t *keysIn, uint32_t *keysOut, uint32_t n,
                           const ScanRes *sres, bool byKey, void *tmp, size_t tmpBytes, hipStream_t s) {
-  hipLaunchKernelGGL(searchKeyKernel, dim3((n + 255) / 256), dim3(256), 0, s, listIn, n, sres, byKey ? 1 : 0, keysIn);
+  const int kmode = getenv("GWA_SEARCH_KEY") ? atoi(getenv("GWA_SEARCH_KEY")) : 1;  // (experiment)
+  hipLaunchKernelGGL(searchKeyKernel, dim3((n + 255) / 256), dim3(256), 0, s, listIn, n, sres, byKey ? kmode : 0, keysIn);
   FCHK(hipGetLastError());
   size_t b = tmpBytes;
-  FCHK(rocprim::radix_sort_pairs(tmp, b, keysIn, keysOut, listIn, listOut, (size_t)n, 0, byKey ? 15 : 32, s));
+  FCHK(rocprim::radix_sort_pairs(tmp, b, keysIn, keysOut, listIn, listOut, (size_t)n, 0, byKey ? 22 : 32, s));
 }
 
 }  // namespace gwa

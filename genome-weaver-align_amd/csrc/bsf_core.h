@@ -1090,7 +1090,7 @@ struct BsfLane {
 
   // ---- FMQuickScan.scanMismatchLocations (S/FMQuickScan.java:66-94) ----
   // uniq != 0: [lb, ub) is one row whose suffix-array value is tp (the FM steps ran in text mode)
-  struct Scan { uint64_t lb, ub, tp; int numMismatches, lmStart, uniq; };
+  struct Scan { uint64_t lb, ub, tp; int numMismatches, lmStart, uniq, firstEmpty; };
 
   // One reference FM step from a single-row interval, read off the text instead of the Occ blocks.
   // For a one-row interval [l, l+1) with SA value p, backwardSearch(c) (A/FMIndexOnOccTable.java:47-51)
@@ -1175,7 +1175,7 @@ struct BsfLane {
     const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
     const uint64_t N = ix.N;
     uint64_t lb = 0, ub = N;
-    int mark = 0, nmm = 0;
+    int mark = 0, nmm = 0, fe = m;
     // longestMatch bookkeeping kept branch-free (loop-carried i1 flags in this divergent loop were
     // mis-lowered by the gfx950 backend in our tests); `have` is an int 0/1.
     int have = 0;
@@ -1245,6 +1245,7 @@ struct BsfLane {
       lmS = better ? mark : lmS;
       lmE = better ? i : lmE;
       have |= empty;
+      fe = (empty && nmm == 0) ? i : fe;
       nmm += empty;
       lb = empty ? 0 : nlb;
       ub = empty ? N : nub;
@@ -1258,7 +1259,7 @@ struct BsfLane {
       lmE = better ? i : lmE;
     }
     Scan s;
-    s.lb = lb; s.ub = ub; s.tp = tp; s.numMismatches = nmm; s.lmStart = lmS; s.uniq = uniq;
+    s.lb = lb; s.ub = ub; s.tp = tp; s.numMismatches = nmm; s.lmStart = lmS; s.uniq = uniq; s.firstEmpty = fe;
     return s;
   }
 
@@ -2127,6 +2128,7 @@ struct BsfLane {
     if (k == 0) { finishQuick(oh); return 0; }
     sr->nmF = sF.numMismatches; sr->lmF = sF.lmStart;
     sr->nmR = sR.numMismatches; sr->lmR = sR.lmStart;
+    sr->feF = sF.firstEmpty; sr->feR = sR.firstEmpty;
     finishQuick(oh);
     return 1;
   }

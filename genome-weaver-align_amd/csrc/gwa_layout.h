@@ -222,6 +222,7 @@ struct ResumeBufs {
 // S/BidirectionalSuffixFilter.java:324-346)
 struct ScanRes {
   int32_t nmF, lmF, nmR, lmR;
+  int32_t feF, feR;  // each strand's first empty step (m: none): the search-list sort key only
 };
 
 // CIGAR op = (len << 3) | type ; type: M0 I1 D2 N3 S4 H5 P6 X7  (A/CIGAR.java:39-47)

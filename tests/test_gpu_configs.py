@@ -47,11 +47,11 @@ def _say(request, msg):
         print("[configs] %s" % msg, flush=True)
 
 
-def _compare(got, exp):
+def _compare(got, exp, what=""):
     if got != exp:
         g, e = got.splitlines(), exp.splitlines()
         bad = [(a, b) for a, b in zip(g, e) if a != b][:3]
-        raise AssertionError("SAM differs: %d vs %d lines; first diffs: %r" % (len(g), len(e), bad))
+        raise AssertionError("SAM differs%s: %d vs %d lines; first diffs: %r" % (what, len(g), len(e), bad))
 
 
 @pytest.fixture(scope="module")
@@ -126,7 +126,8 @@ def _batch_and_check(request, gi, oi, strs, m, k, strategy, n_random):
                        threads=_threads())
     _say(request, "%s k=%g m=%d: %d reads on the GPU (tiers %s, %.1fs), %d compared (%d from tiers >= 1) in %.1fs"
          % (strategy, k, m, n, list(st.tier_reads), t1 - t0, len(samp), len(deep), time.time() - t1))
-    _compare(got, exp)
+    _compare(got, exp, " (compared: %d of %d reads = %d random + every tier >= 1 read, %d of them)"
+             % (len(samp), n, min(n_random, n), len(deep)))
     return st, deep
 
 
