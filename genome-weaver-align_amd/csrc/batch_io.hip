@@ -376,12 +376,13 @@ void launchStats(const OutHeader *oh, uint32_t n, unsigned long long *acc, hipSt
 // The searched reads' order does not change any result (each lane runs its own reads to the end), but
 // it decides which reads share a wavefront.  A read's best-first search starts from seeds given by its
 // quick scan (each strand's numMismatches and longest-match start, S/BidirectionalSuffixFilter.java:
-// 318-341), so reads with the same seeds walk trees of a similar shape: they reach their reports and
-// finish at similar times and the wavefront's lanes stay busy together.  Key (byKey): the
-// longest-match start of the strand with fewer mismatches (4-base buckets), then the two strands'
-// mismatch counts (fewer, more).  !byKey: the read index (a deep tier's list back in input order).
-// A stable radix sort keeps input order inside a key.  Measured per 10M C2 reads (search ms, hg19 /
-// hg19r): unsorted 89.0 / 158.5, this key 77.2 / 142.1; DESIGN.md §4 has the other keys tried.
+// 318-341), so reads whose scans match alike walk search trees of a similar shape: they reach their
+// reports and finish at similar times, and the lanes of a wavefront take the same paths through a
+// micro-step together.  Key (byKey), of the strand with fewer mismatches ("lo"; forward on a tie): its
+// longest-match start, then both strands' mismatch counts, then its first empty step (2-base buckets).
+// !byKey: the read index (a deep tier's list back in input order).  A stable radix sort keeps input
+// order inside a key.  Measured per 10M C2 reads (first-tier search ms, hg19 / hg19r): unsorted
+// 89.0 / 132.0, this key 65.3 / 111.1; DESIGN.md §4 lists the keys tried.
 __global__ void searchKeyKernel(const uint32_t *list, uint32_t n, const ScanRes *sres, int byKey, uint32_t *keys) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -393,9 +394,8 @@ __global__ void searchKeyKernel(const uint32_t *list, uint32_t n, const ScanRes 
   const ScanRes q = sres[r];
   const bool f = q.nmF <= q.nmR;
   const uint32_t lo = (uint32_t)(f ? q.nmF : q.nmR) & 15, hi = (uint32_t)(f ? q.nmR : q.nmF) & 15;
-  const uint32_t lm = (uint32_t)(f ? q.lmF : q.lmR) & 511;
-  keys[i] = (lm >> 2) << 8 | lo << 4 | hi;
-  if (byKey == 2) keys[i] = keys[i] << 7 | (((uint32_t)(f ? q.feF : q.feR) & 511) >> 2);
+  const uint32_t lm = (uint32_t)(f ? q.lmF : q.lmR) & 511, fe = (uint32_t)(f ? q.feF : q.feR) & 511;
+  keys[i] = (((lm >> 1) << 4 | lo) << 4 | hi) << 8 | fe >> 1;
 }
 
 size_t sortSearchListTmpBytes(uint32_t n) {
@@ -407,11 +407,10 @@ size_t sortSearchListTmpBytes(uint32_t n) {
 
 void launchSortSearchList(const uint32_t *listIn, uint32_t *listOut, uint32_t *keysIn, uint32_t *keysOut, uint32_t n,
                           const ScanRes *sres, bool byKey, void *tmp, size_t tmpBytes, hipStream_t s) {
-  const int kmode = getenv("GWA_SEARCH_KEY") ? atoi(getenv("GWA_SEARCH_KEY")) : 1;  // (experiment)
-  hipLaunchKernelGGL(searchKeyKernel, dim3((n + 255) / 256), dim3(256), 0, s, listIn, n, sres, byKey ? kmode : 0, keysIn);
+  hipLaunchKernelGGL(searchKeyKernel, dim3((n + 255) / 256), dim3(256), 0, s, listIn, n, sres, byKey ? 1 : 0, keysIn);
   FCHK(hipGetLastError());
   size_t b = tmpBytes;
-  FCHK(rocprim::radix_sort_pairs(tmp, b, keysIn, keysOut, listIn, listOut, (size_t)n, 0, byKey ? 22 : 32, s));
+  FCHK(rocprim::radix_sort_pairs(tmp, b, keysIn, keysOut, listIn, listOut, (size_t)n, 0, byKey ? 24 : 32, s));
 }
 
 }  // namespace gwa

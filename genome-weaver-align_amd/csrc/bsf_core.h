@@ -1175,7 +1175,7 @@ struct BsfLane {
     const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
     const uint64_t N = ix.N;
     uint64_t lb = 0, ub = N;
-    int mark = 0, nmm = 0, fe = m;
+    int mark = 0, nmm = 0, fe = m;  // fe: the first empty step (the search-list sort key)
     // longestMatch bookkeeping kept branch-free (loop-carried i1 flags in this divergent loop were
     // mis-lowered by the gfx950 backend in our tests); `have` is an int 0/1.
     int have = 0;
