@@ -1171,96 +1171,107 @@ struct BsfLane {
     return j < L ? j : L;
   }
 
-  GWA_HD Scan quickScan(int strand) {
+  // One strand's FMQuickScan as a resumable loop: quickScan runs qsStep until qsMore is false; the
+  // persistent quick-scan kernel runs one qsStep per lane per iteration, so a lane whose read is done
+  // takes the next read instead of waiting for its wavefront's slowest scan (search_kernels.h).
+  struct QS {
+    uint64_t lb, ub, tp;
+    // fe: the first empty step (the search-list sort key).  longestMatch bookkeeping kept branch-free
+    // (loop-carried i1 flags in this divergent loop were mis-lowered by the gfx950 backend in our
+    // tests); `have` is an int 0/1.  Text mode: once the interval is a single row [lb, lb + 1) with SA
+    // value tp, each further step is one text character compare (textBefore), run 32 at a time by
+    // textRun; uniq is an int 0/1 for the same reason as have.
+    int i, mark, nmm, fe, have, lmS, lmE, uniq, strand;
+  };
+  GWA_HD void qsBegin(QS &s, int strand) const {
+    s.lb = 0; s.ub = ix.N; s.tp = 0;
+    s.i = 0; s.mark = 0; s.nmm = 0; s.fe = m; s.have = 0; s.lmS = 0; s.lmE = 0; s.uniq = 0; s.strand = strand;
+  }
+  // The scan stops at its (k+1)-th empty interval: the caller only reads numMismatches <= k and,
+  // under that condition, longestMatch (S/BidirectionalSuffixFilter.java:324-345), so a scan past
+  // k + 1 mismatches cannot change the result (the wrong strand of a read stops after ~3 restarts).
+  GWA_HD bool qsMore(const QS &s) const { return s.i < m && s.nmm <= k; }
+  GWA_HD void qsStep(QS &s) {
+    const int strand = s.strand;
     const int fm = strand == 0 ? 1 : 0;  // forwardSearch on FORWARD uses the reverse index (:134-137)
     const uint64_t N = ix.N;
-    uint64_t lb = 0, ub = N;
-    int mark = 0, nmm = 0, fe = m;  // fe: the first empty step (the search-list sort key)
-    // longestMatch bookkeeping kept branch-free (loop-carried i1 flags in this divergent loop were
-    // mis-lowered by the gfx950 backend in our tests); `have` is an int 0/1.
-    int have = 0;
-    int lmS = 0, lmE = 0;
-    // text mode: once the interval is a single row [lb, lb + 1) with SA value tp, each further step
-    // is one text character compare (textBefore), run 32 at a time by textRun.  uniq is an int 0/1
-    // for the same reason as have.
-    int uniq = 0;
-    uint64_t tp = 0;
     const int K = ix.kmerK;
-    int i = 0;
-    // The scan stops at its (k+1)-th empty interval: the caller only reads numMismatches <= k and,
-    // under that condition, longestMatch (S/BidirectionalSuffixFilter.java:324-345), so a scan past
-    // k + 1 mismatches cannot change the result (the wrong strand of a read stops after ~3 restarts).
-    while (i < m && nmm <= k) {
-      // at a restart from [0, N) (mark == i), the k-mer table answers the next K steps at once
-      // when none of them is empty; otherwise the steps below run one by one
-      if (K > 0 && i == mark && i + K <= m) {
-        const uint32_t key = qWindow(strand, i, K);
-        const uint64_t e = ix.kmer[fm][key];
-        ++kmerLookups;
-        if (e != 0) {
-          lb = e & 0xFFFFFFFFULL;
-          ub = e >> 32;
-          quickSteps += K;
-          shortSteps += K;
-          i += K;
-          const int u = ub - lb == 1 ? 1 : 0;
-          if (u) { tp = ix.sa[fm][lb]; ++saReads; }
-          uniq = u;
-          continue;
-        }
+    // at a restart from [0, N) (mark == i), the k-mer table answers the next K steps at once
+    // when none of them is empty; otherwise the steps below run one by one
+    if (K > 0 && s.i == s.mark && s.i + K <= m) {
+      const uint32_t key = qWindow(strand, s.i, K);
+      const uint64_t e = ix.kmer[fm][key];
+      ++kmerLookups;
+      if (e != 0) {
+        s.lb = e & 0xFFFFFFFFULL;
+        s.ub = e >> 32;
+        quickSteps += K;
+        shortSteps += K;
+        s.i += K;
+        const int u = s.ub - s.lb == 1 ? 1 : 0;
+        if (u) { s.tp = ix.sa[fm][s.lb]; ++saReads; }
+        s.uniq = u;
+        return;
       }
-      uint64_t nlb = lb, nub = ub;
-      int empty;
-      if (uniq) {
-        const int L = m - i < 32 ? m - i : 32;
-        const int j = textRun(fm, tp, strand, i, L);
-        ++textRuns;
-        tp = tp >= (uint64_t)j ? tp - j : tp + N - j;  // j hits, each moving to SA value tp - 1 (cyclic)
-        i += j;
-        quickSteps += j;
-        shortSteps += j;
-        if (j == L) continue;
-        ++quickSteps;  // the step at i: BWT character != read base, empty interval
-        ++shortSteps;
-        empty = 1;
-      } else {
-        const int ch = q(strand, i);
-        // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
-        // one 64-B block when lb and ub share a 128-position window
-        Block B;
-        loadBlock(ix.occ[fm], lb >> 7, B);
+    }
+    const int i = s.i;
+    uint64_t nlb = s.lb, nub = s.ub;
+    int empty;
+    if (s.uniq) {
+      const int L = m - i < 32 ? m - i : 32;
+      const int j = textRun(fm, s.tp, strand, i, L);
+      ++textRuns;
+      s.tp = s.tp >= (uint64_t)j ? s.tp - j : s.tp + N - j;  // j hits, each moving to SA value tp - 1 (cyclic)
+      s.i += j;
+      quickSteps += j;
+      shortSteps += j;
+      if (j == L) return;
+      ++quickSteps;  // the step at i: BWT character != read base, empty interval
+      ++shortSteps;
+      empty = 1;
+    } else {
+      const int ch = q(strand, i);
+      // backwardSearch(ch, si) = C[ch] + getOcc(ch, lb|ub) (A/FMIndexOnOccTable.java:47-51);
+      // one 64-B block when lb and ub share a 128-position window
+      Block B;
+      loadBlock(ix.occ[fm], s.lb >> 7, B);
+      ++blocks;
+      nlb = ix.C[ch] + rankOne(B, s.lb, ch);
+      if ((s.ub >> 7) != (s.lb >> 7)) {
+        loadBlock(ix.occ[fm], s.ub >> 7, B);
         ++blocks;
-        nlb = ix.C[ch] + rankOne(B, lb, ch);
-        if ((ub >> 7) != (lb >> 7)) {
-          loadBlock(ix.occ[fm], ub >> 7, B);
-          ++blocks;
-        }
-        nub = ix.C[ch] + rankOne(B, ub, ch);
-        ++quickSteps;
-        tr(16 + strand, (uint32_t)(i | (ch << 16)), (uint32_t)nlb, (uint32_t)nub);
-        empty = nlb >= nub ? 1 : 0;
-        if (!empty && nub - nlb == 1) { tp = ix.sa[fm][nlb]; ++saReads; uniq = 1; }
       }
-      const int better = empty & ((have ^ 1) | ((lmE - lmS) < (i - mark) ? 1 : 0));
-      lmS = better ? mark : lmS;
-      lmE = better ? i : lmE;
-      have |= empty;
-      fe = (empty && nmm == 0) ? i : fe;
-      nmm += empty;
-      lb = empty ? 0 : nlb;
-      ub = empty ? N : nub;
-      mark = empty ? i + 1 : mark;
-      uniq = empty ? 0 : uniq;
-      ++i;
+      nub = ix.C[ch] + rankOne(B, s.ub, ch);
+      ++quickSteps;
+      tr(16 + strand, (uint32_t)(i | (ch << 16)), (uint32_t)nlb, (uint32_t)nub);
+      empty = nlb >= nub ? 1 : 0;
+      if (!empty && nub - nlb == 1) { s.tp = ix.sa[fm][nlb]; ++saReads; s.uniq = 1; }
     }
-    {
-      const int better = (have ^ 1) | ((lmE - lmS) < (i - mark) ? 1 : 0);
-      lmS = better ? mark : lmS;
-      lmE = better ? i : lmE;
-    }
-    Scan s;
-    s.lb = lb; s.ub = ub; s.tp = tp; s.numMismatches = nmm; s.lmStart = lmS; s.uniq = uniq; s.firstEmpty = fe;
-    return s;
+    const int ii = s.i;  // (the text branch moved i past its matches to the empty step)
+    const int better = empty & ((s.have ^ 1) | ((s.lmE - s.lmS) < (ii - s.mark) ? 1 : 0));
+    s.lmS = better ? s.mark : s.lmS;
+    s.lmE = better ? ii : s.lmE;
+    s.have |= empty;
+    s.fe = (empty && s.nmm == 0) ? ii : s.fe;
+    s.nmm += empty;
+    s.lb = empty ? 0 : nlb;
+    s.ub = empty ? N : nub;
+    s.mark = empty ? ii + 1 : s.mark;
+    s.uniq = empty ? 0 : s.uniq;
+    s.i = ii + 1;
+  }
+  GWA_HD Scan qsEnd(const QS &s) const {
+    const int better = (s.have ^ 1) | ((s.lmE - s.lmS) < (s.i - s.mark) ? 1 : 0);
+    Scan r;
+    r.lb = s.lb; r.ub = s.ub; r.tp = s.tp; r.numMismatches = s.nmm; r.lmStart = better ? s.mark : s.lmS; r.uniq = s.uniq;
+    r.firstEmpty = s.fe;
+    return r;
+  }
+  GWA_HD Scan quickScan(int strand) {
+    QS s;
+    qsBegin(s, strand);
+    while (qsMore(s)) qsStep(s);
+    return qsEnd(s);
   }
 
   // ---- hits (R/ReadHit.java) ----
@@ -2107,6 +2118,15 @@ struct BsfLane {
   // Phase 1 (fm_quickscan kernel): N check, FMQuickScan on both strands, exact hits.
   // Returns 1 when the read needs the best-first search; otherwise the result is final.
   GWA_HD int quickPhase(ScanRes *sr, OutHeader *oh, const OutSlots &os, uint32_t rd_) {
+    if (!quickOpen(oh)) return 0;
+    Scan sF = quickScan(0);
+    if (sF.numMismatches == 0) { reportExact(sF, 0, oh, os, rd_); return 0; }
+    Scan sR = quickScan(1);
+    return quickClose(sF.numMismatches, sF.lmStart, sF.firstEmpty, sR, sr, oh, os, rd_);
+  }
+  // quickPhase's opening: the header's search fields cleared, the read words loaded; false = the read
+  // has more N than k mismatches (its result is final)
+  GWA_HD bool quickOpen(OutHeader *oh) {
     oh->fmSearches = 0;
     oh->states = 0;
     oh->searchBlocks = 0;
@@ -2117,18 +2137,19 @@ struct BsfLane {
     oh->ovfWhat = 0;
     oh->nChains = oh->nHits = oh->nCigar = 0;
     oh->status = ST_UNMAPPED;
-    {
-      const int countN = loadWords(pw0, pw1);
-      if (countN > k) { finishQuick(oh); return 0; }
-    }
-    Scan sF = quickScan(0);
-    if (sF.numMismatches == 0) { reportExact(sF, 0, oh, os, rd_); return 0; }
-    Scan sR = quickScan(1);
+    const int countN = loadWords(pw0, pw1);
+    if (countN > k) { finishQuick(oh); return false; }
+    return true;
+  }
+  // quickPhase's close after both strands (strand 0 inexact: its numMismatches, longest-match start,
+  // first empty step); 1 = the read needs the best-first search
+  GWA_HD int quickClose(int nmF, int lmF, int feF, const Scan &sR, ScanRes *sr, OutHeader *oh, const OutSlots &os,
+                        uint32_t rd_) {
     if (sR.numMismatches == 0) { reportExact(sR, 1, oh, os, rd_); return 0; }
     if (k == 0) { finishQuick(oh); return 0; }
-    sr->nmF = sF.numMismatches; sr->lmF = sF.lmStart;
+    sr->nmF = nmF; sr->lmF = lmF;
     sr->nmR = sR.numMismatches; sr->lmR = sR.lmStart;
-    sr->feF = sF.firstEmpty; sr->feR = sR.firstEmpty;
+    sr->feF = feF; sr->feR = sR.firstEmpty;
     finishQuick(oh);
     return 1;
   }
