@@ -1200,6 +1200,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
       // (the second tier's input has no resume records -- the first tier does not suspend -- so its
       // list may be reordered; deeper tiers find their records by list position)
+      // (key order for the second tier too: C4 tier 1 184 ms against 117 ms, hg19r's 21.9 against 23.5)
       if (sortLists && n > 1 && (t == 0 || (t == 1 && resIn.cap == 0))) sortList(t == 0);
       // the budget and this tier's scratch / resume allocations as one step per device (released
       // before the launch: the memory is allocated by then, so the next batch's budget sees it)
