@@ -721,6 +721,7 @@ static bool batchHead(gwa_index *ix, const gwa_config_t *cfg, uint32_t n, gwa_ba
   // a wavefront runs its parked reports once they are waitQ16/16 of its live lanes; the default is
   // set with the NFA size in batchTail (DESIGN.md §4 sweeps)
   sc.waitQ16 = getenv("GWA_WAITQ16") ? atoi(getenv("GWA_WAITQ16")) : 0;
+  sc.refillMin = 1;  // (per tier: gwa_batch_run)
   sc.textSearch = (cfg->num_split <= 1 && !getenv("GWA_NO_TEXT")) ? 1 : 0;
   sc.runAheadMax = getenv("GWA_RUNAHEAD") ? atoi(getenv("GWA_RUNAHEAD")) : 4;
   sc.textCache = getenv("GWA_TEXT_CACHE") ? atoi(getenv("GWA_TEXT_CACHE")) : 0;
@@ -1290,6 +1291,20 @@ int gwa_batch_run(gwa_batch_t *b) {
       allocLock.unlock();
       HIPCHK(hipEventRecord(e1, s));
       const OutSlots os = outSlots(b);
+      // The first tier's wavefronts take new reads for their idle lanes only once most of their lanes
+      // are idle (SearchConfig::refillMin), as a run of consecutive reads of the key-sorted list: the
+      // lanes of a wavefront then hold reads of one key and step together, and they run their reports
+      // later, when more of them are parked (waitQ16).  First-tier search ms (hg19 / hg19r / C4 per 1M):
+      // lane by lane, waitQ16 14 (8): 65.0 / 110.9 / 100.3; refill 48 (C4 32): 46.2 / 80.9 / 90.5;
+      // with waitQ16 16: 41.7 / 89.8 / 99.7; 15 and refill 56 (kept): 44.0 / 84.6; C4 waitQ16 12:
+      // 84.9.  Deeper tiers keep lane-by-lane refills and their thresholds (C4 tier 1: 114.7 ms; 120.2
+      // at refill 32; 172 at waitQ16 16).  SAM identical throughout.  GWA_REFILL sets the first tier's
+      // threshold (1: lane by lane, A/B runs); GWA_WAITQ16 still sets every tier's.
+      SearchConfig tcfg = b->scfg;
+      if (tb == 0 && !sf) {
+        tcfg.refillMin = getenv("GWA_REFILL") ? atoi(getenv("GWA_REFILL")) : b->R >= 8 ? 32 : 56;
+        if (!getenv("GWA_WAITQ16")) tcfg.waitQ16 = b->R >= 8 ? 12 : 15;
+      }
 #ifdef GWA_PROF
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
@@ -1299,7 +1314,7 @@ int gwa_batch_run(gwa_batch_t *b) {
                        (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s, (uint32_t *)d_prof);
       else
-        launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres,
+        launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, tcfg, b->st, rv, b->d_sres,
                      b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb,
                      b->d_list[cur ^ 1], ovfCount, ovfBits, rb, s, (uint32_t *)d_prof, -1);
       {
@@ -1333,7 +1348,7 @@ int gwa_batch_run(gwa_batch_t *b) {
                        (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s);
       else
-        launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, b->scfg, b->st, rv, b->d_sres, b->d_list[cur], n,
+        launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, tcfg, b->st, rv, b->d_sres, b->d_list[cur], n,
                      scr.p, stride, caps, b->d_oh, os, ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1],
                      ovfCount, ovfBits, rb, s);
 #endif

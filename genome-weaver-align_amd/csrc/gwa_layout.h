@@ -82,6 +82,9 @@ struct SearchConfig {
   // 1: every text-mode FM step reads the text through the lane's one-word cache (BsfLane::refCodeCached),
   // kept across search steps (the states of one read mostly walk one text neighbourhood)
   int32_t textCache;
+  // scheduler: a wavefront's idle lanes take new reads once at least this many are idle (or all its
+  // live lanes are); 1 = each lane as soon as it is idle
+  int32_t refillMin;
 };
 
 // Read batch as resident in HBM: one byte code (0..4) per base; every read starts at a 16-B

@@ -137,7 +137,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GWA_SE
   for (;;) {
     const bool need = phase == IDLE;
     const uint64_t needMask = __ballot(need);
-    if (needMask) {
+    // (cfg.refillMin > 1: the idle lanes wait until that many are idle or every live lane is)
+    if (needMask && (cfg.refillMin <= 1 || __popcll(needMask) >= cfg.refillMin ||
+                     needMask == __ballot(phase != EXHAUSTED))) {
       const int lid = __lane_id();
       const int leader = __ffsll((long long)needMask) - 1;
       uint32_t base = 0;
