@@ -1201,7 +1201,8 @@ int gwa_batch_run(gwa_batch_t *b) {
       if (++launches > 96) throw std::runtime_error("search capacity growth did not converge");
       // (the second tier's input has no resume records -- the first tier does not suspend -- so its
       // list may be reordered; deeper tiers find their records by list position)
-      // (key order for the second tier too: C4 tier 1 184 ms against 117 ms, hg19r's 21.9 against 23.5)
+      // (key order for the second tier too: C4 tier 1 184 ms against 117 ms, 178-193 ms with
+      // wavefront-wide refills as well; hg19r's 21.9 against 23.5 ms)
       if (sortLists && n > 1 && (t == 0 || (t == 1 && resIn.cap == 0))) sortList(t == 0);
       // the budget and this tier's scratch / resume allocations as one step per device (released
       // before the launch: the memory is allocated by then, so the next batch's budget sees it)
@@ -1305,6 +1306,7 @@ int gwa_batch_run(gwa_batch_t *b) {
         tcfg.refillMin = getenv("GWA_REFILL") ? atoi(getenv("GWA_REFILL")) : b->R >= 8 ? 32 : 56;
         if (!getenv("GWA_WAITQ16")) tcfg.waitQ16 = b->R >= 8 ? 12 : 15;
       }
+
 #ifdef GWA_PROF
       uint64_t *d_prof = nullptr;
       HIPCHK(hipMalloc(&d_prof, (size_t)lanes * PR_N * 8));
