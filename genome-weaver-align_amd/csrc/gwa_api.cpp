@@ -1077,6 +1077,11 @@ int gwa_batch_run(gwa_batch_t *b) {
     if (!sf)
       launchQuickscan(qwFor(b->maxM), ix->view, b->scfg, rv, b->d_sres, b->d_oh, outSlots(b), b->d_list[0],
                       b->d_count, s);
+    // -m sf, k >= 4 (R >= 8): the quick scan of every read for the search-list key only (see sortLists
+    // below).  C4 (1M reads): search 17.8 -> 13.7 ms for a 1.6 ms scan; at k = 2 (C2 -m sf, 2M reads)
+    // 9.8 -> 9.4 ms for a 1.8 ms scan, so k <= 3 batches keep input order.
+    const bool sfSort = sf && b->R >= 8 && !(getenv("GWA_SEARCH_SORT") && atoi(getenv("GWA_SEARCH_SORT")) == 0);
+    if (sfSort) launchKeyscan(qwFor(b->maxM), ix->view, b->scfg, rv, b->d_sres, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e1, s));
     uint32_t nSearch = b->n;
@@ -1095,7 +1100,11 @@ int gwa_batch_run(gwa_batch_t *b) {
     // input order (in the first tier's completion order, i.e. key order, the heavy reads of one key
     // would crowd the same wavefronts: C4 tier 1 158 ms against 112 ms).  -m sf searches every read in
     // input order.  GWA_SEARCH_SORT=0: no sorting (A/B runs).
-    const bool sortLists = !sf && !(getenv("GWA_SEARCH_SORT") && atoi(getenv("GWA_SEARCH_SORT")) == 0);
+    // -m sf (round 6): every read is searched, and a wavefront takes 64 reads at a time and runs each
+    // to its end (sf_search_kernel), so the first tier's list of all reads is sorted by the same key,
+    // from a quick scan that only computes it (launchKeyscan).
+    const bool sortLists = !(getenv("GWA_SEARCH_SORT") && atoi(getenv("GWA_SEARCH_SORT")) == 0);
+    bool sfSorted = false;  // (-m sf: the first tier reads the sorted list, not d_all)
     const int m = std::max(b->maxM, 1);
     int t = 0, regrow = 0, launches = 0;
     // Reads that overflow the last tier rerun on it with the exceeded capacities doubled (OV_* bits
@@ -1182,12 +1191,12 @@ int gwa_batch_run(gwa_batch_t *b) {
       return caps;
     };
     // the search-list sort (tier 0: by quick-scan key; the second tier: input order)
-    auto sortList = [&](bool byKey) {
+    auto sortList = [&](bool byKey, const uint32_t *in) {
       const size_t tb = sortSearchListTmpBytes(n);
       uint32_t *keys = bAlloc<uint32_t>(2 * (size_t)n);
       void *tmp = batchMalloc(std::max<size_t>(tb, 64));
       HIPCHK(hipEventRecord(e1, s));
-      launchSortSearchList(b->d_list[cur], b->d_list[cur ^ 1], keys, keys + n, n, b->d_sres, byKey, tmp, tb, s);
+      launchSortSearchList(in, b->d_list[cur ^ 1], keys, keys + n, n, b->d_sres, byKey, tmp, tb, s);
       HIPCHK(hipEventRecord(e2, s));
       HIPCHK(hipStreamSynchronize(s));
       float ms = 0;
@@ -1203,7 +1212,12 @@ int gwa_batch_run(gwa_batch_t *b) {
       // list may be reordered; deeper tiers find their records by list position)
       // (key order for the second tier too: C4 tier 1 184 ms against 117 ms, 178-193 ms with
       // wavefront-wide refills as well; hg19r's 21.9 against 23.5 ms)
-      if (sortLists && n > 1 && (t == 0 || (t == 1 && resIn.cap == 0))) sortList(t == 0);
+      if (sfSort && n > 1 && t == 0 && regrow == 0) {
+        sortList(true, b->d_all);
+        sfSorted = true;
+      } else if (sortLists && n > 1 && ((t == 0 && !sf) || (t == 1 && resIn.cap == 0))) {
+        sortList(t == 0, b->d_list[cur]);
+      }
       // the budget and this tier's scratch / resume allocations as one step per device (released
       // before the launch: the memory is allocated by then, so the next batch's budget sees it)
       std::unique_lock<std::mutex> allocLock(g_allocMu[ix->device & 63]);
@@ -1313,7 +1327,7 @@ int gwa_batch_run(gwa_batch_t *b) {
       HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)lanes * PR_N * 8, s));
       if (sf)
         launchSfSearch(b->R, qwFor(b->maxM), b->sfWrap, lanes, ix->view, b->scfg, b->st, rv,
-                       (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
+                       (t == 0 && regrow == 0 && !sfSorted) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s, (uint32_t *)d_prof);
       else
         launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, tcfg, b->st, rv, b->d_sres,
@@ -1347,7 +1361,7 @@ int gwa_batch_run(gwa_batch_t *b) {
 #else
       if (sf)
         launchSfSearch(b->R, qwFor(b->maxM), b->sfWrap, lanes, ix->view, b->scfg, b->st, rv,
-                       (t == 0 && regrow == 0) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
+                       (t == 0 && regrow == 0 && !sfSorted) ? b->d_all : b->d_list[cur], n, scr.p, stride, caps, b->d_oh, os,
                        ix->d_chrRank, b->d_count + 8 + tb, b->d_list[cur ^ 1], ovfCount, ovfBits, s);
       else
         launchSearch(b->R, qwFor(b->maxM), deepLds ? 2 : (tb == 0 || hybrid) ? 1 : 0, lanes, ix->view, tcfg, b->st, rv, b->d_sres, b->d_list[cur], n,

@@ -305,6 +305,14 @@ void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const
   else launchQuickscanT<16>(ix, cfg, reads, sres, oh, os, searchList, searchCount, s, trace, traceRead);
 }
 
+void launchKeyscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres,
+                   hipStream_t s) {
+  if (reads.n == 0) return;
+  if (QW == 4) launchKeyscanT<4>(ix, cfg, reads, sres, s);
+  else if (QW == 8) launchKeyscanT<8>(ix, cfg, reads, sres, s);
+  else launchKeyscanT<16>(ix, cfg, reads, sres, s);
+}
+
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg,
                   const StairTables &st, const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n,
                   uint8_t *scratch, uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,

@@ -13,6 +13,9 @@ struct Caps;
 void launchQuickscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
                      const OutSlots &os, uint32_t *searchList, uint32_t *searchCount,
                      hipStream_t s, uint32_t *trace = nullptr, int traceRead = -1);
+// -m sf: every read's quick-scan result into sres (the search-list key), nothing else written
+void launchKeyscan(int QW, const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres,
+                   hipStream_t s);
 void launchSearch(int R, int QW, int ldsHeap, uint32_t lanes, const IndexView &ix, const SearchConfig &cfg, const StairTables &st,
                   const ReadsView &reads, const ScanRes *sres, const uint32_t *list, uint32_t n, uint8_t *scratch,
                   uint64_t laneStride, const Caps &caps, OutHeader *oh, const OutSlots &os,

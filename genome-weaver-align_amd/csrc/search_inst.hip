@@ -10,6 +10,7 @@
 namespace gwa {
 GWA_SEARCH_INSTANCE(template, GWA_QW, GWA_R)
 #if GWA_R == 4
+template void launchKeyscanT<GWA_QW>(const IndexView &, const SearchConfig &, const ReadsView &, ScanRes *, hipStream_t);
 template void launchQuickscanT<GWA_QW>(const IndexView &, const SearchConfig &, const ReadsView &, ScanRes *, OutHeader *,
                                        const OutSlots &, uint32_t *, uint32_t *, hipStream_t, uint32_t *, int);
 #endif

@@ -55,6 +55,31 @@ __global__ void __launch_bounds__(256) fm_quickscan_kernel(IndexView ix, SearchC
   waveAppend(need, r, searchList, searchCount);
 }
 
+// -m sf: the quick scan's per-strand result of every read, for the search-list key only (no output is
+// written: the SuffixFilter search decides every read).  Reads too long or with more N than k keep a
+// key of zeros.
+template <int QW>
+__global__ void __launch_bounds__(256) fm_keyscan_kernel(IndexView ix, SearchConfig cfg, ReadsView reads, ScanRes *sres) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= reads.n) return;
+  ScanRes q{};
+  const int m = (int)reads.len[r];
+  if (m <= 32 * QW) {
+    StairTables st{};
+    LaneMem<4> L{};
+    Caps caps{};
+    BsfLane<4, QW> lane(ix, cfg, st, L, caps);
+    lane.initRead(reads.codes + reads.off[r], m);
+    if (lane.loadWords(lane.pw0, lane.pw1) <= lane.k) {
+      const auto sF = lane.quickScan(0);
+      const auto sR = lane.quickScan(1);
+      q.nmF = sF.numMismatches; q.lmF = sF.lmStart; q.feF = sF.firstEmpty;
+      q.nmR = sR.numMismatches; q.lmR = sR.lmStart; q.feR = sR.firstEmpty;
+    }
+  }
+  sres[r] = q;
+}
+
 #ifndef GWA_SEARCH_WAVES
 #define GWA_SEARCH_WAVES 2
 #endif
@@ -420,6 +445,11 @@ sf_search_kernel(IndexView ix, SearchConfig cfg, StairTables st, ReadsView reads
 
 
 template <int QW>
+void launchKeyscanT(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, hipStream_t s) {
+  hipLaunchKernelGGL(fm_keyscan_kernel<QW>, dim3((reads.n + 255) / 256), dim3(256), 0, s, ix, cfg, reads, sres);
+}
+
+template <int QW>
 void launchQuickscanT(const IndexView &ix, const SearchConfig &cfg, const ReadsView &reads, ScanRes *sres, OutHeader *oh,
                       const OutSlots &os, uint32_t *searchList, uint32_t *searchCount, hipStream_t s, uint32_t *trace,
                       int traceRead) {
@@ -487,6 +517,8 @@ void launchSfSearchQR(bool wrap, uint32_t lanes, const IndexView &ix, const Sear
   GWA_SEARCH_INSTANCE(extern template, QW_, 8)                                                                    \
   GWA_SEARCH_INSTANCE(extern template, QW_, 16)                                                                   \
   GWA_SEARCH_INSTANCE(extern template, QW_, 32)                                                                   \
+  extern template void launchKeyscanT<QW_>(const IndexView &, const SearchConfig &, const ReadsView &, ScanRes *,     \
+                                           hipStream_t);                                                             \
   extern template void launchQuickscanT<QW_>(const IndexView &, const SearchConfig &, const ReadsView &, ScanRes *, \
                                              OutHeader *, const OutSlots &, uint32_t *, uint32_t *, hipStream_t,   \
                                              uint32_t *, int);
