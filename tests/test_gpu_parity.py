@@ -694,3 +694,22 @@ def test_gpu_cyclic_sa_known_answers(gwa):
         gi = gwa.FMIndexOnGenome.buildFromCodes(codes, ["t"], [len(codes)])
         assert list(gi.suffixArray(0)) == case["expect"], case["name"]
         gi.close()
+
+
+@pytest.mark.parametrize("strat,k", [("bsf", 2.0), ("bsf", 4.0), ("sf", 4.0)])
+def test_search_order_and_refill_do_not_change_results(random_pair, monkeypatch, strat, k):
+    # round 6: the first-tier search list sorted by quick-scan key (radix sort) and the wavefront-wide
+    # refill threshold only reorder work; with both off (GWA_SEARCH_SORT=0, GWA_REFILL=1: input
+    # order, a lane refilled as soon as it empties) the SAM text is byte-identical and equals the oracle
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    seqs, rn = synth.reads(codes, lengths, 3000, 100, int(k) + 1, config_id=61)
+    strs = synth.to_strings(seqs)
+    reads = [(rn[i], strs[i], "I" * 100) for i in range(len(strs))]
+    cfg = gwa.AlignmentConfig(k=k, strategy=strat)
+    sam_default = gwa.aligner(gi, cfg).align_batch(reads)
+    monkeypatch.setenv("GWA_SEARCH_SORT", "0")
+    monkeypatch.setenv("GWA_REFILL", "1")
+    sam_plain = gwa.aligner(gi, cfg).align_batch(reads)
+    assert sam_default == sam_plain
+    assert sam_default == oi.align(reads, O.OrcConfig.default(k=k, strategy=["bsf", "sf"].index(strat)))
