@@ -991,7 +991,10 @@ static uint32_t tierValue(const char *var, int t, uint32_t def) {
 static uint64_t scratchBudget(size_t held) {
   size_t freeB = 0, totalB = 0;
   if (hipMemGetInfo(&freeB, &totalB) != hipSuccess) return 16ull << 30;
-  return std::min<uint64_t>(64ull << 30, ((uint64_t)freeB + held + devCacheIdle()) / 2);
+  uint64_t cap = 64ull << 30;
+  if (const char *e = getenv("GWA_SCRATCH_BUDGET_MB"))  // tests: concurrent batches under a small budget
+    if (atoll(e) > 0) cap = std::min<uint64_t>(cap, (uint64_t)atoll(e) << 20);
+  return std::min<uint64_t>(cap, ((uint64_t)freeB + held + devCacheIdle()) / 2);
 }
 
 // the batch's output slots + pool (gwa_layout.h OutSlots); pool counters at d_count[12..14]

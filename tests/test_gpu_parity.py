@@ -713,3 +713,43 @@ def test_search_order_and_refill_do_not_change_results(random_pair, monkeypatch,
     sam_plain = gwa.aligner(gi, cfg).align_batch(reads)
     assert sam_default == sam_plain
     assert sam_default == oi.align(reads, O.OrcConfig.default(k=k, strategy=["bsf", "sf"].index(strat)))
+
+
+@pytest.mark.parametrize("strat,arena", [("bsf", "64"), ("sf", None)])
+def test_concurrent_batches_small_scratch_budget(random_pair, monkeypatch, strat, arena):
+    # batches of several host threads size their search scratch at the same time.
+    # Under a small budget (GWA_SCRATCH_BUDGET_MB), and for -m bsf with a small first-tier arena so that
+    # reads overflow into the deep tiers, three concurrent batches all finish and equal the oracle.
+    import threading
+    import gwa
+    codes, names, lengths, gi, oi = random_pair
+    monkeypatch.setenv("GWA_SCRATCH_BUDGET_MB", "256")
+    if arena:
+        monkeypatch.setenv("GWA_TIER_ARENA", arena)
+    cfg = gwa.AlignmentConfig(k=4.0, strategy=strat)
+    batches = []
+    for j in range(3):
+        seqs, rn = synth.reads(codes, lengths, 1500, 100, 5, config_id=70 + j)
+        strs = synth.to_strings(seqs)
+        batches.append([("b%d_%s" % (j, rn[i]), strs[i], "I" * 100) for i in range(len(strs))])
+    got, deep, errs = [None] * 3, [0] * 3, []
+
+    def work(j):
+        try:
+            b = gwa.Batch(gi, cfg, batches[j])
+            b.run()
+            deep[j] = sum(list(b.stats().tier_reads)[1:])
+            got[j] = b.results()[0]
+            b.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+    th = [threading.Thread(target=work, args=(j,)) for j in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+    if arena:
+        assert min(deep) > 0, deep  # every batch ran deep tiers
+    for j in range(3):
+        assert got[j] == oi.align(batches[j], O.OrcConfig.default(k=4.0, strategy=["bsf", "sf"].index(strat)))
